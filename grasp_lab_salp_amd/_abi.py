@@ -1,0 +1,91 @@
+"""Python mirror of the C ABI in include/salp.h (struct layout, field ids).
+
+Kept as the single Python-side description of the boundary; tests check it
+against the names exported by libsalp.so (salp_field_name) so the two cannot
+drift apart silently.
+"""
+import ctypes
+
+ABI_VERSION = 1
+MAX_OBSTACLES = 4
+OBS_DIM_MAX = 6 + 2 * MAX_OBSTACLES
+
+
+class SalpParams(ctypes.Structure):
+    """Constructor arguments of Nozzle / Robot / SalpRobotEnv (include/salp.h)."""
+
+    _fields_ = [
+        ("nozzle_length1", ctypes.c_double),
+        ("nozzle_length2", ctypes.c_double),
+        ("nozzle_length3", ctypes.c_double),
+        ("nozzle_area", ctypes.c_double),
+        ("nozzle_mass", ctypes.c_double),
+        ("dry_mass", ctypes.c_double),
+        ("init_length", ctypes.c_double),
+        ("init_width", ctypes.c_double),
+        ("max_contraction", ctypes.c_double),
+        ("density", ctypes.c_double),
+        ("init_angle1", ctypes.c_double),
+        ("init_angle2", ctypes.c_double),
+        ("obstacle_radius", ctypes.c_double),
+        ("width", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+        ("num_obstacles", ctypes.c_int32),
+        ("max_cycles", ctypes.c_int32),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+def default_params(**overrides):
+    """Canonical configuration of src/train_robot.py:11-21 (make_env)."""
+    p = SalpParams(
+        nozzle_length1=0.05, nozzle_length2=0.05, nozzle_length3=0.05, nozzle_area=0.00016,
+        nozzle_mass=1.0, dry_mass=1.0, init_length=0.3, init_width=0.15, max_contraction=0.06,
+        density=1000.0, init_angle1=0.0, init_angle2=0.0, obstacle_radius=0.2, width=900,
+        height=700, num_obstacles=2, max_cycles=500)
+    for k, v in overrides.items():
+        if not hasattr(p, k):
+            raise TypeError(f"unknown SalpParams field {k!r}")
+        setattr(p, k, v)
+    return p
+
+
+def _vec(name):
+    return [f"{name}{i}" for i in range(3)]
+
+
+# Order == enum SalpField in include/salp.h
+FIELDS = (
+    _vec("v") + _vec("w") + _vec("acc") + _vec("alpha") + _vec("eta") + _vec("pw") + _vec("pos")
+    + _vec("ang") + _vec("ppos") + _vec("pang") + _vec("avgv") + _vec("avgw")
+    + ["length", "width", "volume", "prev_volume", "com", "com_rate", "com_acc"]
+    + _vec("prev_I") + ["geom32", "pvol32"]
+    + ["cycle_time", "time", "refill_time", "jet_time", "coast_time", "contraction",
+       "contract_rate", "release_rate", "phase", "cycle"]
+    + ["angle1", "angle2", "yaw", "prev_yaw", "turn_time"]
+    + ["target0", "target1"] + [f"obst{i}" for i in range(2 * MAX_OBSTACLES)]
+    + ["n_obst", "prev_dist", "prev_a2"]
+    + ["ep_len", "ep_return", "path_len", "last_px", "last_py", "sum_a0", "sum_a1", "sum_abs_a2",
+       "sum_vel", "init_dist"] + [f"sum_r{i}" for i in range(7)]
+    + ["act0", "act1", "act2", "pending", "step_count", "episode"]
+)
+NUM_FIELDS = len(FIELDS)
+FIELD = {name: i for i, name in enumerate(FIELDS)}
+
+INFO_KEYS = (
+    "rewards/track", "rewards/heading", "rewards/smooth", "rewards/yaw", "rewards/time",
+    "rewards/sideslip", "rewards/obstacle",
+    "path_length", "direct_distance", "path_efficiency", "final_distance", "initial_distance",
+    "avg_compression", "avg_coast_time", "avg_nozzle_angle", "avg_velocity",
+    "avg_rewards_track", "avg_rewards_heading", "avg_rewards_smooth", "avg_rewards_yaw",
+    "avg_rewards_time", "avg_rewards_sideslip", "avg_rewards_obstacle",
+    "ep_return", "ep_len", "has_metrics", "hit_obstacle",
+)
+INFO_DIM = len(INFO_KEYS)
+INFO = {k: i for i, k in enumerate(INFO_KEYS)}
+REWARD_COMPONENT_KEYS = INFO_KEYS[:7]
+EPISODE_METRIC_KEYS = INFO_KEYS[7:23]
+
+PHASES = ("REFILL", "JET", "COAST", "REST")  # src/robot.py:252-257

@@ -1,0 +1,279 @@
+/*
+ * salp_math.h — portable, bit-reproducible fp64/fp32 elementary functions and
+ * the NumPy/OpenBLAS evaluation-order primitives the reference's arithmetic
+ * goes through.
+ *
+ * Why this exists.  The reference (Avielstein/GRASP_LAB_SALP, src/ Python) runs
+ * its physics through NumPy.  Two facts about that arithmetic shape the design:
+ *
+ *  1. Every 3x3 product, mat-vec and norm in the reference is a BLAS call on
+ *     NumPy 2.2 + OpenBLAS, and those kernels accumulate with FMA in a fixed
+ *     order.  Probed in the build container (tests/test_numpy_semantics.py pins
+ *     it):
+ *        np.linalg.norm(v)      = sqrt(fma(v2,v2, fma(v1,v1, v0*v0)))
+ *        (A @ B)[i,j]           = fma(A[i,2],B[2,j], fma(A[i,1],B[1,j], A[i,0]*B[0,j]))
+ *        (A.T @ v)[i]           = fma(A[2,i],v2, fma(A[1,i],v1, A[0,i]*v0))
+ *        (A @ v)[i]  (C-contig) = fma(A[i,2],v2, fma(A[i,0],v0, A[i,1]*v1))
+ *        np.linalg.solve(diag(d), b) = b / d
+ *     The np_* helpers below restate exactly those orders, so the device
+ *     kernel and the CPU oracle both reproduce the reference's rounding.
+ *
+ *  2. The nozzle inverse kinematics (src/robot.py:71-98) feed float32
+ *     cos/sin of the yaw into arcsin() right next to |x|=1, where a one-ulp
+ *     change of the float32 inputs moves angle1 by ~1e-4 rad.  NumPy's float32
+ *     sin/cos is its own SIMD algorithm (Cody-Waite reduction + minimax
+ *     polynomials evaluated with fmaf; NumPy >= 1.22 loops_trigonometric) and
+ *     is not correctly rounded, so sm_np_sincosf() restates that published
+ *     algorithm bit for bit (0 mismatches over the action range, see tests).
+ *
+ * The fp64 transcendentals (sin, cos, tan, atan, atan2, asin, acos) are
+ * fdlibm-style (Cody-Waite pi/2 reduction, minimax kernels) and accurate to
+ * about one ulp; glibc/SVML, which the reference uses, are not reproducible
+ * bit for bit on a GPU, so oracle-vs-reference agreement is ulp-level there
+ * (DESIGN.md §Parity).  The device kernel and the oracle include THIS header,
+ * so device-vs-oracle comparisons are exact.
+ *
+ * Everything here uses only IEEE-754 correctly rounded operations (+ - * /
+ * sqrt, fma, rint, conversions) so gcc (x86-64, -ffp-contract=off) and hipcc
+ * (gfx950, -ffp-contract=off) produce identical bits.
+ */
+#ifndef SALP_MATH_H
+#define SALP_MATH_H
+
+#include <stdint.h>
+
+#if defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define SM_QUAL __host__ __device__ static inline
+#else
+#include <math.h>
+#include <string.h>
+#define SM_QUAL static inline
+#endif
+
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+
+/* ---------------------------------------------------------------- bits */
+SM_QUAL uint64_t sm_d2u(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (uint64_t)__double_as_longlong(x);
+#else
+    uint64_t u; memcpy(&u, &x, 8); return u;
+#endif
+}
+SM_QUAL double sm_u2d(uint64_t u) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __longlong_as_double((long long)u);
+#else
+    double x; memcpy(&x, &u, 8); return x;
+#endif
+}
+SM_QUAL int32_t sm_hi(double x) { return (int32_t)(sm_d2u(x) >> 32); }
+
+SM_QUAL double sm_fma(double a, double b, double c) { return fma(a, b, c); }
+SM_QUAL float sm_fmaf(float a, float b, float c) { return fmaf(a, b, c); }
+
+/* ------------------------------------------------ NumPy/OpenBLAS orders */
+/* np.linalg.norm of a 3-vector / 2-vector (ddot FMA chain, then sqrt). */
+SM_QUAL double np_norm3(double a, double b, double c) {
+    return sqrt(sm_fma(c, c, sm_fma(b, b, a * a)));
+}
+SM_QUAL double np_norm2(double a, double b) { return sqrt(sm_fma(b, b, a * a)); }
+/* One entry of a 3x3 @ 3x3 product, or of a transposed mat-vec. */
+SM_QUAL double np_dot_fwd(double a0, double a1, double a2, double b0, double b1, double b2) {
+    return sm_fma(a2, b2, sm_fma(a1, b1, a0 * b0));
+}
+/* One row of a C-contiguous 3x3 @ 3-vector (dgemv) product. */
+SM_QUAL double np_matvec_row(double a0, double a1, double a2, double v0, double v1, double v2) {
+    return sm_fma(a2, v2, sm_fma(a0, v0, a1 * v1));
+}
+/* Correctly rounded x**3 (glibc pow agrees except in ~1e-3 of inputs). */
+SM_QUAL double sm_cube(double x) {
+    double p = x * x, pe = sm_fma(x, x, -p);
+    double h = p * x, he = sm_fma(p, x, -h);
+    return h + sm_fma(pe, x, he);
+}
+
+/* ------------------------------------------- NumPy float32 sin / cos */
+/* NumPy SIMD float32 sin/cos: quadrant by x*(2/pi) rounded with the 1.5*2^23
+ * magic constant, three-constant Cody-Waite reduction with fmaf, and the
+ * degree-8 cos / degree-9 sin minimax polynomials in r^2. */
+SM_QUAL void sm_np_sincosf(float x, float* s_out, float* c_out) {
+    const float two_over_pi = 0x1.45f306p-01f;
+    const float magic = 0x1.800000p+23f;
+    const float pio2_hi = -0x1.921fb0p+00f;
+    const float pio2_med = -0x1.5110b4p-22f;
+    const float pio2_lo = -0x1.846988p-48f;
+    float q = x * two_over_pi;
+    q = q + magic;
+    q = q - magic;
+    float r = sm_fmaf(q, pio2_hi, x);
+    r = sm_fmaf(q, pio2_med, r);
+    r = sm_fmaf(q, pio2_lo, r);
+    float r2 = r * r;
+    float c = sm_fmaf(0x1.98e616p-16f, r2, -0x1.6c06dcp-10f);
+    c = sm_fmaf(c, r2, 0x1.55553cp-05f);
+    c = sm_fmaf(c, r2, -0x1.000000p-01f);
+    c = sm_fmaf(c, r2, 0x1.000000p+00f);
+    float s = sm_fmaf(0x1.7d3bbcp-19f, r2, -0x1.a06bbap-13f);
+    s = sm_fmaf(s, r2, 0x1.11119ap-07f);
+    s = sm_fmaf(s, r2, -0x1.555556p-03f);
+    s = s * r2;
+    s = sm_fmaf(s, r, r);
+    int iq = (int)q;
+    /* sine: quadrant iq; cosine: quadrant iq+1 */
+    float sv = (iq & 1) ? c : s;
+    if (iq & 2) sv = -sv;
+    int iqc = iq + 1;
+    float cv = (iqc & 1) ? c : s;
+    if (iqc & 2) cv = -cv;
+    *s_out = sv;
+    *c_out = cv;
+}
+
+/* ------------------------------------------------- fp64 sin/cos (fdlibm) */
+SM_QUAL double sm_ksin(double x, double y, int iy) {
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    double z = x * x, w = z * z;
+    double r = S2 + z * (S3 + z * S4) + z * w * (S5 + z * S6);
+    double v = z * x;
+    if (iy == 0) return x + v * (S1 + z * r);
+    return x - ((z * (0.5 * y - v * r) - y) - v * S1);
+}
+SM_QUAL double sm_kcos(double x, double y) {
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    double z = x * x, w = z * z;
+    double r = z * (C1 + z * (C2 + z * C3)) + w * w * (C4 + z * (C5 + z * C6));
+    double hz = 0.5 * z;
+    w = 1.0 - hz;
+    return w + (((1.0 - w) - hz) + (z * r - x * y));
+}
+/* Cody-Waite reduction for |x| < 2^20*pi/2 (fdlibm __ieee754_rem_pio2,
+ * medium case).  Returns n with x = n*pi/2 + (y0 + y1). */
+SM_QUAL int sm_rem_pio2(double x, double* y0, double* y1) {
+    const double invpio2 = 6.36619772367581382433e-01,
+                 pio2_1 = 1.57079632673412561417e+00, pio2_1t = 6.07710050650619224932e-11,
+                 pio2_2 = 6.07710050630396597660e-11, pio2_2t = 2.02226624879595063154e-21,
+                 pio2_3 = 2.02226624871116645580e-21, pio2_3t = 8.47842766036889956997e-32;
+    double fn = rint(x * invpio2);
+    double r = x - fn * pio2_1;
+    double w = fn * pio2_1t;
+    double y = r - w;
+    int j = (sm_hi(x) >> 20) & 0x7ff;
+    int i = j - ((sm_hi(y) >> 20) & 0x7ff);
+    if (i > 16) {
+        double t = r;
+        w = fn * pio2_2;
+        r = t - w;
+        w = fn * pio2_2t - ((t - r) - w);
+        y = r - w;
+        i = j - ((sm_hi(y) >> 20) & 0x7ff);
+        if (i > 49) {
+            t = r;
+            w = fn * pio2_3;
+            r = t - w;
+            w = fn * pio2_3t - ((t - r) - w);
+            y = r - w;
+        }
+    }
+    *y0 = y;
+    *y1 = (r - y) - w;
+    return (int)fn;
+}
+SM_QUAL void sm_sincos(double x, double* s_out, double* c_out) {
+    int32_t ix = sm_hi(x) & 0x7fffffff;
+    if (ix <= 0x3fe921fb) { /* |x| <= pi/4 */
+        *s_out = sm_ksin(x, 0.0, 0);
+        *c_out = sm_kcos(x, 0.0);
+        return;
+    }
+    double y0, y1;
+    int n = sm_rem_pio2(x, &y0, &y1);
+    double s = sm_ksin(y0, y1, 1), c = sm_kcos(y0, y1);
+    switch (n & 3) {
+        case 0: *s_out = s; *c_out = c; break;
+        case 1: *s_out = c; *c_out = -s; break;
+        case 2: *s_out = -s; *c_out = -c; break;
+        default: *s_out = -c; *c_out = s; break;
+    }
+}
+SM_QUAL double sm_sin(double x) { double s, c; sm_sincos(x, &s, &c); return s; }
+SM_QUAL double sm_cos(double x) { double s, c; sm_sincos(x, &s, &c); return c; }
+SM_QUAL double sm_tan(double x) { double s, c; sm_sincos(x, &s, &c); return s / c; }
+
+/* ----------------------------------------------------- atan family */
+SM_QUAL double sm_atan(double x) {
+    const double atanhi[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01,
+                              9.82793723247329054082e-01, 1.57079632679489655800e+00};
+    const double atanlo[4] = {2.26987774529616870924e-17, 3.06161699786838301793e-17,
+                              1.39033110312309984516e-17, 6.12323399573676603587e-17};
+    const double aT0 = 3.33333333333329318027e-01, aT1 = -1.99999999998764832476e-01,
+                 aT2 = 1.42857142725034663711e-01, aT3 = -1.11111104054623557880e-01,
+                 aT4 = 9.09088713343650656196e-02, aT5 = -7.69187620504482999495e-02,
+                 aT6 = 6.66107313738753120669e-02, aT7 = -5.83357013379057348645e-02,
+                 aT8 = 4.97687799461593236017e-02, aT9 = -3.65315727442169155270e-02,
+                 aT10 = 1.62858201153657823623e-02;
+    int32_t hx = sm_hi(x), ix = hx & 0x7fffffff;
+    int id;
+    if (ix >= 0x44100000) { /* |x| >= 2^66 */
+        double z = atanhi[3] + atanlo[3];
+        return hx < 0 ? -z : z;
+    }
+    if (ix < 0x3fdc0000) { /* |x| < 0.4375 */
+        if (ix < 0x3e400000) return x;
+        id = -1;
+    } else {
+        x = fabs(x);
+        if (ix < 0x3ff30000) {
+            if (ix < 0x3fe60000) { id = 0; x = (2.0 * x - 1.0) / (2.0 + x); }
+            else { id = 1; x = (x - 1.0) / (x + 1.0); }
+        } else {
+            if (ix < 0x40038000) { id = 2; x = (x - 1.5) / (1.0 + 1.5 * x); }
+            else { id = 3; x = -1.0 / x; }
+        }
+    }
+    double z = x * x, w = z * z;
+    double s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+    double s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+    if (id < 0) return x - x * (s1 + s2);
+    z = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    return hx < 0 ? -z : z;
+}
+SM_QUAL double sm_atan2(double y, double x) {
+    const double pi = 3.1415926535897931160e+00, pi_o_2 = 1.5707963267948965580e+00,
+                 pi_lo = 1.2246467991473531772e-16;
+    if (x != x || y != y) return x + y;
+    if (x == 1.0) return sm_atan(y);
+    int32_t hx = sm_hi(x), hy = sm_hi(y);
+    int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+    if (y == 0.0) {
+        switch (m) {
+            case 0: case 1: return y;
+            case 2: return pi;
+            default: return -pi;
+        }
+    }
+    if (x == 0.0) return hy < 0 ? -pi_o_2 : pi_o_2;
+    int32_t ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
+    int k = (iy - ix) >> 20;
+    double z;
+    if (k > 60) { z = pi_o_2 + 0.5 * pi_lo; m &= 1; }
+    else if (hx < 0 && k < -60) z = 0.0;
+    else z = sm_atan(fabs(y / x));
+    switch (m) {
+        case 0: return z;
+        case 1: return -z;
+        case 2: return pi - (z - pi_lo);
+        default: return (z - pi_lo) - pi;
+    }
+}
+SM_QUAL double sm_asin(double x) { return sm_atan2(x, sqrt((1.0 - x) * (1.0 + x))); }
+SM_QUAL double sm_acos(double x) { return sm_atan2(sqrt((1.0 - x) * (1.0 + x)), x); }
+
+#endif /* SALP_MATH_H */

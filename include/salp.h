@@ -1,0 +1,202 @@
+/*
+ * salp.h — C ABI of the MI355X-native batched SALP simulator (libsalp.so).
+ *
+ * Drop-in boundary.  The reference (Avielstein/GRASP_LAB_SALP) exposes the hot
+ * path only as Python objects:
+ *
+ *   SalpRobotEnv(render_mode, width, height, robot, num_obstacles, obstacle_radius)
+ *       src/salp_robot_env.py:35          -> salp_create / SalpParams
+ *   SalpRobotEnv.reset(seed, options) -> (obs, {})
+ *       src/salp_robot_env.py:114-155     -> salp_reset / salp_reset_to
+ *   SalpRobotEnv.step(action) -> (obs, reward, terminated, truncated, info)
+ *       src/salp_robot_env.py:196-299     -> salp_step
+ *   Robot(dry_mass, init_length, init_width, max_contraction, nozzle),
+ *   Nozzle(length1, length2, length3, area, mass), Robot.set_environment,
+ *   Nozzle.set_angles        src/robot.py:20-21, 261-262, 443-449, 50-60
+ *                                         -> SalpParams fields
+ *   Robot / Nozzle state attributes (src/robot.py:261-412)
+ *                                         -> salp_get_state / salp_set_state
+ *   SB3 VecEnv rollout collection around env.step (src/train_robot.py:26,
+ *   src/train_robot_recurrent_ppo.py:65)  -> salp_rollout (rollout-buffer fill)
+ *
+ * The Python host layer (grasp_lab_salp_amd/) binds these with ctypes; the
+ * reference-side binding a maintainer would add is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Every array argument is a caller-owned DEVICE pointer (e.g. a torch
+ *    tensor's data_ptr()) on the handle's device; `stream` is a hipStream_t
+ *    (NULL = the legacy default stream).  Calls only enqueue work: nothing
+ *    synchronises and nothing allocates after salp_create.
+ *  - Return value: 0 on success, a negative SALP_E* code on error; the
+ *    message is available from salp_last_error(h) (h may be NULL for errors
+ *    raised by salp_create).  No C++ exception crosses this boundary.
+ *  - A handle is not thread-safe: one handle per GPU per process.
+ *  - Physics is fp64 end to end (the reference is NumPy fp64); observations
+ *    are float32 exactly as the reference returns them; rewards are fp64.
+ */
+#ifndef SALP_H
+#define SALP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SALP_ABI_VERSION 1
+
+#define SALP_MAX_OBSTACLES 4
+#define SALP_OBS_DIM_MAX (6 + 2 * SALP_MAX_OBSTACLES)
+/* info_out row: 7 reward components, 16 episode metrics, ep return, ep length,
+ * has_metrics flag, terminal hit_obstacle flag (see SALP_INFO_* below). */
+#define SALP_INFO_DIM 27
+
+#define SALP_OK 0
+#define SALP_EINVAL -1
+#define SALP_EHIP -2
+#define SALP_ENOMEM -3
+
+/* Constructor arguments of the reference objects.  Constants that the
+ * reference hard-codes (dt=0.01, drag/added-mass coefficients, the polynomial
+ * cycle-time fits, masses of buoy/skin/tube) are not parameters there and are
+ * not parameters here either. */
+typedef struct SalpParams {
+    /* Nozzle(length1, length2, length3, area, mass)   src/robot.py:20-21 */
+    double nozzle_length1, nozzle_length2, nozzle_length3, nozzle_area, nozzle_mass;
+    /* Robot(dry_mass, init_length, init_width, max_contraction, nozzle)
+     *                                                  src/robot.py:261-262 */
+    double dry_mass, init_length, init_width, max_contraction;
+    /* Robot.set_environment(density)                  src/robot.py:443-449 */
+    double density;
+    /* Nozzle.set_angles(angle1, angle2) done by make_env before the env is
+     * built (src/train_robot.py:16)                   src/robot.py:50-60 */
+    double init_angle1, init_angle2;
+    /* SalpRobotEnv(width, height, num_obstacles, obstacle_radius)
+     *                                                  src/salp_robot_env.py:35 */
+    double obstacle_radius;
+    int32_t width, height, num_obstacles;
+    int32_t max_cycles; /* timeout, hard-coded 500 at src/salp_robot_env.py:274 */
+} SalpParams;
+
+typedef struct SalpEnv SalpEnv; /* opaque handle */
+
+/* Rollout-buffer fill targets for salp_rollout (all device pointers, rows
+ * indexed [slot][env], slot = completed-step counter of that env modulo
+ * `capacity`).  Any pointer may be NULL to skip that output. */
+typedef struct SalpRolloutBuffers {
+    int64_t capacity;      /* slots per env                                  */
+    float* obs;            /* [capacity][n_envs][obs_dim]  obs AFTER the step  */
+    float* actions;        /* [capacity][n_envs][3]                            */
+    float* rewards;        /* [capacity][n_envs]  (float32, SB3 buffer dtype)  */
+    uint8_t* dones;        /* [capacity][n_envs]  bit0 terminated, bit1 truncated */
+    int64_t* steps_done;   /* [n_envs] completed env-steps counter (in/out)    */
+} SalpRolloutBuffers;
+
+/* ------------------------------------------------------------ lifecycle */
+int salp_abi_version(void);
+void salp_default_params(SalpParams* p); /* canonical make_env config */
+int salp_create(const SalpParams* p, int64_t n_envs, uint64_t seed, int64_t env_id_offset,
+                int device, SalpEnv** out);
+int salp_destroy(SalpEnv* h);
+const char* salp_last_error(const SalpEnv* h);
+int64_t salp_num_envs(const SalpEnv* h);
+int salp_obs_dim(const SalpEnv* h);
+
+/* -------------------------------------------------------------- env API */
+/* reset(): per masked env (mask NULL = all) draw target + obstacles from the
+ * env's Philox stream, Robot.reset(), episode trackers; writes obs rows of
+ * masked envs.  obs_out [n_envs][obs_dim] (NULL allowed). */
+int salp_reset(SalpEnv* h, const uint8_t* mask, float* obs_out, void* stream);
+/* reset() with the target / obstacles given by the caller (the reference
+ * draws them from the global np.random; parity tests inject them).
+ * targets [n][2], obstacles [n][SALP_MAX_OBSTACLES][2], n_obstacles [n]. */
+int salp_reset_to(SalpEnv* h, const uint8_t* mask, const float* targets, const float* obstacles,
+                  const int32_t* n_obstacles, float* obs_out, void* stream);
+/* One SalpRobotEnv.step per env (one breathing cycle each).
+ * actions [n][3] float32 in the action box; outputs may be NULL.
+ * auto_reset != 0: envs that end are reset (SB3 VecEnv semantics); their
+ * obs_out row is then the reset observation and terminal_obs_out [n][obs_dim]
+ * receives the final observation.  info_out [n][SALP_INFO_DIM] fp64. */
+int salp_step(SalpEnv* h, const float* actions, float* obs_out, double* reward_out,
+              uint8_t* terminated_out, uint8_t* truncated_out, int auto_reset,
+              float* terminal_obs_out, double* info_out, void* stream);
+/* Synthetic random-action rollout, chained per lane: every env runs exactly
+ * `tick_budget` physics ticks (dt=0.01 each), completing as many env-steps as
+ * fit, with actions ~ U(action box) from Philox(seed; env id, step index) and
+ * auto-reset (Philox targets/obstacles).  A cycle cut by the budget resumes
+ * on the next call; results do not depend on how ticks are split. */
+int salp_rollout(SalpEnv* h, int64_t tick_budget, const SalpRolloutBuffers* buf, void* stream);
+/* Same random actions, lock-step: every env performs exactly n_steps
+ * env-steps (one full cycle each) with auto-reset.  rewards_out [n] = sum. */
+int salp_step_random(SalpEnv* h, int32_t n_steps, double* reward_sum_out, void* stream);
+
+/* --------------------------------------------------------- state access */
+/* State is a struct-of-arrays of SALP_NUM_FIELDS fp64 rows of n_envs each:
+ * state[field * n_envs + env].  Integer and float32 quantities are stored
+ * exactly as doubles. */
+int salp_num_fields(void);
+const char* salp_field_name(int field);
+int salp_get_state(SalpEnv* h, double* state_out, void* stream);
+int salp_set_state(SalpEnv* h, const double* state_in, void* stream);
+/* Device-side self-test of salp_math.h: out[i] = f(x[i]) for f in
+ * {sin, cos, tan, atan2(x, y), asin, acos, cube, np_cosf, np_sinf}.
+ * x, y [n]; out [9][n]. */
+int salp_math_selftest(const double* x, const double* y, int64_t n, double* out, void* stream);
+
+/* State fields.  Names follow the reference attribute they hold. */
+enum SalpField {
+    /* Robot vectors (src/robot.py:358-374), body frame unless noted */
+    SALP_F_V0 = 0, SALP_F_V1, SALP_F_V2,                  /* velocity */
+    SALP_F_W0, SALP_F_W1, SALP_F_W2,                      /* angular_velocity */
+    SALP_F_ACC0, SALP_F_ACC1, SALP_F_ACC2,                /* acceleration */
+    SALP_F_ALPHA0, SALP_F_ALPHA1, SALP_F_ALPHA2,          /* angular_acceleration */
+    SALP_F_ETA0, SALP_F_ETA1, SALP_F_ETA2,                /* euler_angle (world) */
+    SALP_F_PW0, SALP_F_PW1, SALP_F_PW2,                   /* position_world */
+    SALP_F_POS0, SALP_F_POS1, SALP_F_POS2,                /* position */
+    SALP_F_ANG0, SALP_F_ANG1, SALP_F_ANG2,                /* angle */
+    SALP_F_PPOS0, SALP_F_PPOS1, SALP_F_PPOS2,             /* prev_position */
+    SALP_F_PANG0, SALP_F_PANG1, SALP_F_PANG2,             /* prev_angle */
+    SALP_F_AVGV0, SALP_F_AVGV1, SALP_F_AVGV2,             /* avg_cycle_velocity */
+    SALP_F_AVGW0, SALP_F_AVGW1, SALP_F_AVGW2,             /* avg_cycle_angular_velocity */
+    /* body geometry / mass properties (src/robot.py:325-339) */
+    SALP_F_LENGTH, SALP_F_WIDTH, SALP_F_VOLUME, SALP_F_PREV_VOLUME,
+    SALP_F_COM, SALP_F_COM_RATE, SALP_F_COM_ACC,          /* x components (y,z == 0) */
+    SALP_F_PREV_I0, SALP_F_PREV_I1, SALP_F_PREV_I2,       /* diag(prev_I) */
+    /* NumPy dtype of length/width/volume (1 = np.float32, see DESIGN.md
+     * §NEP 50) and of prev_water_volume */
+    SALP_F_GEOM32, SALP_F_PVOL32,
+    /* cycle (src/robot.py:311-322) */
+    SALP_F_CYCLE_TIME, SALP_F_TIME, SALP_F_REFILL_TIME, SALP_F_JET_TIME, SALP_F_COAST_TIME,
+    SALP_F_CONTRACTION, SALP_F_CONTRACT_RATE, SALP_F_RELEASE_RATE, SALP_F_PHASE, SALP_F_CYCLE,
+    /* nozzle (src/robot.py:30-44) */
+    SALP_F_ANGLE1, SALP_F_ANGLE2, SALP_F_YAW, SALP_F_PREV_YAW, SALP_F_TURN_TIME,
+    /* env (src/salp_robot_env.py:114-155) */
+    SALP_F_TARGET0, SALP_F_TARGET1,
+    SALP_F_OBST0, SALP_F_OBST_END = SALP_F_OBST0 + 2 * SALP_MAX_OBSTACLES - 1,
+    SALP_F_N_OBST, SALP_F_PREV_DIST, SALP_F_PREV_A2,
+    /* episode trackers (src/salp_robot_env.py:145-153, 399-447) */
+    SALP_F_EP_LEN, SALP_F_EP_RETURN, SALP_F_PATH_LEN, SALP_F_LAST_PX, SALP_F_LAST_PY,
+    SALP_F_SUM_A0, SALP_F_SUM_A1, SALP_F_SUM_ABS_A2, SALP_F_SUM_VEL, SALP_F_INIT_DIST,
+    SALP_F_SUM_R0, SALP_F_SUM_R_END = SALP_F_SUM_R0 + 6,
+    /* in-flight env-step (action of the cycle being simulated) + RNG counters */
+    SALP_F_ACT0, SALP_F_ACT1, SALP_F_ACT2, SALP_F_PENDING,
+    SALP_F_STEP_COUNT, SALP_F_EPISODE,
+    SALP_NUM_FIELDS
+};
+
+/* info_out columns */
+enum SalpInfo {
+    SALP_INFO_R_TRACK = 0, SALP_INFO_R_HEADING, SALP_INFO_R_SMOOTH, SALP_INFO_R_YAW,
+    SALP_INFO_R_TIME, SALP_INFO_R_SIDESLIP, SALP_INFO_R_OBSTACLE,
+    SALP_INFO_PATH_LENGTH, SALP_INFO_DIRECT_DISTANCE, SALP_INFO_PATH_EFFICIENCY,
+    SALP_INFO_FINAL_DISTANCE, SALP_INFO_INITIAL_DISTANCE, SALP_INFO_AVG_COMPRESSION,
+    SALP_INFO_AVG_COAST_TIME, SALP_INFO_AVG_NOZZLE_ANGLE, SALP_INFO_AVG_VELOCITY,
+    SALP_INFO_AVG_R_TRACK, SALP_INFO_AVG_R_HEADING, SALP_INFO_AVG_R_SMOOTH, SALP_INFO_AVG_R_YAW,
+    SALP_INFO_AVG_R_TIME, SALP_INFO_AVG_R_SIDESLIP, SALP_INFO_AVG_R_OBSTACLE,
+    SALP_INFO_EP_RETURN, SALP_INFO_EP_LEN, SALP_INFO_HAS_METRICS, SALP_INFO_HIT_OBSTACLE
+};
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SALP_H */

@@ -1,0 +1,147 @@
+"""ctypes wrapper of the CPU oracle (oracle/libsalp_oracle.so).
+
+TEST INFRASTRUCTURE ONLY — imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, never by the product package.  See
+oracle/salp_oracle.c for what is restated and where it is pinned.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from grasp_lab_salp_amd._abi import (INFO_DIM, MAX_OBSTACLES, NUM_FIELDS, OBS_DIM_MAX,
+                                     SalpParams, default_params)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libsalp_oracle.so")
+
+_lib = None
+
+
+def build(force=False):
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.POINTER
+        d, f, u8, i32, i64, u32 = (ctypes.c_double, ctypes.c_float, ctypes.c_uint8,
+                                   ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32)
+        sp = P(SalpParams)
+        L.oracle_num_fields.restype = ctypes.c_int
+        L.oracle_init.argtypes = [sp, i64, P(d)]
+        L.oracle_reset_to.argtypes = [sp, i64, P(d), P(u8), P(f), P(f), P(i32), P(f), ctypes.c_int]
+        L.oracle_reset.argtypes = [sp, i64, P(d), P(u8), ctypes.c_uint64, i64, P(f), ctypes.c_int]
+        L.oracle_step.argtypes = [sp, i64, P(d), P(f), P(f), P(d), P(u8), P(u8), ctypes.c_int,
+                                  P(f), P(d), P(i64), ctypes.c_uint64, i64, ctypes.c_int]
+        L.oracle_step_random.argtypes = [sp, i64, P(d), i32, ctypes.c_uint64, i64, P(d),
+                                         ctypes.c_int]
+        L.oracle_step_random.restype = i64
+        L.oracle_robot_trace.argtypes = [sp, P(f), ctypes.c_int, P(d), i64]
+        L.oracle_robot_trace.restype = i64
+        L.oracle_math_selftest.argtypes = [P(d), P(d), i64, P(d)]
+        L.oracle_philox.argtypes = [u32] * 6 + [P(u32)]
+        if L.oracle_num_fields() != NUM_FIELDS:
+            raise RuntimeError("oracle / _abi field count mismatch")
+        _lib = L
+    return _lib
+
+
+def _p(a, ct):
+    return None if a is None else a.ctypes.data_as(ctypes.POINTER(ct))
+
+
+class Oracle:
+    """Batch of reference-equivalent envs on the CPU; state is [NUM_FIELDS, n]."""
+
+    def __init__(self, params=None, n_envs=1, seed=0, env_offset=0):
+        self.params = params if params is not None else default_params()
+        self.n = int(n_envs)
+        self.seed = int(seed)
+        self.env_offset = int(env_offset)
+        self.obs_dim = 6 + 2 * self.params.num_obstacles
+        self.state = np.zeros((NUM_FIELDS, self.n), np.float64)
+        lib().oracle_init(ctypes.byref(self.params), self.n, _p(self.state, ctypes.c_double))
+
+    def _mask(self, mask):
+        if mask is None:
+            return None
+        return np.ascontiguousarray(mask, dtype=np.uint8)
+
+    def reset(self, mask=None):
+        obs = np.zeros((self.n, self.obs_dim), np.float32)
+        m = self._mask(mask)
+        lib().oracle_reset(ctypes.byref(self.params), self.n, _p(self.state, ctypes.c_double),
+                           _p(m, ctypes.c_uint8), self.seed, self.env_offset,
+                           _p(obs, ctypes.c_float), self.obs_dim)
+        return obs
+
+    def reset_to(self, targets, obstacles, n_obstacles, mask=None):
+        t = np.ascontiguousarray(targets, np.float32).reshape(self.n, 2)
+        o = np.zeros((self.n, MAX_OBSTACLES, 2), np.float32)
+        ob = np.asarray(obstacles, np.float32).reshape(self.n, -1, 2)
+        o[:, :ob.shape[1]] = ob
+        k = np.ascontiguousarray(n_obstacles, np.int32).reshape(self.n)
+        obs = np.zeros((self.n, self.obs_dim), np.float32)
+        m = self._mask(mask)
+        lib().oracle_reset_to(ctypes.byref(self.params), self.n, _p(self.state, ctypes.c_double),
+                              _p(m, ctypes.c_uint8), _p(t, ctypes.c_float), _p(o, ctypes.c_float),
+                              _p(k, ctypes.c_int32), _p(obs, ctypes.c_float), self.obs_dim)
+        return obs
+
+    def step(self, actions, auto_reset=False):
+        a = np.ascontiguousarray(actions, np.float32).reshape(self.n, 3)
+        out = dict(obs=np.zeros((self.n, self.obs_dim), np.float32),
+                   reward=np.zeros(self.n, np.float64),
+                   terminated=np.zeros(self.n, np.uint8), truncated=np.zeros(self.n, np.uint8),
+                   terminal_obs=np.zeros((self.n, self.obs_dim), np.float32),
+                   info=np.zeros((self.n, INFO_DIM), np.float64),
+                   ticks=np.zeros(self.n, np.int64))
+        lib().oracle_step(ctypes.byref(self.params), self.n, _p(self.state, ctypes.c_double),
+                          _p(a, ctypes.c_float), _p(out["obs"], ctypes.c_float),
+                          _p(out["reward"], ctypes.c_double), _p(out["terminated"], ctypes.c_uint8),
+                          _p(out["truncated"], ctypes.c_uint8), int(bool(auto_reset)),
+                          _p(out["terminal_obs"], ctypes.c_float), _p(out["info"], ctypes.c_double),
+                          _p(out["ticks"], ctypes.c_int64), self.seed, self.env_offset,
+                          self.obs_dim)
+        return out
+
+    def step_random(self, n_steps, threads=0):
+        rs = np.zeros(self.n, np.float64)
+        ticks = lib().oracle_step_random(ctypes.byref(self.params), self.n,
+                                         _p(self.state, ctypes.c_double), int(n_steps), self.seed,
+                                         self.env_offset, _p(rs, ctypes.c_double), int(threads))
+        return rs, int(ticks)
+
+
+def robot_trace(actions, params=None, max_rows=200000):
+    params = params if params is not None else default_params()
+    a = np.ascontiguousarray(actions, np.float32).reshape(-1, 3)
+    out = np.zeros((max_rows, 29), np.float64)
+    n = lib().oracle_robot_trace(ctypes.byref(params), _p(a, ctypes.c_float), len(a),
+                                 _p(out, ctypes.c_double), max_rows)
+    if n < 0:
+        raise RuntimeError("trace buffer too small")
+    return out[:n]
+
+
+def math_selftest(x, y):
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    out = np.zeros((9, len(x)), np.float64)
+    lib().oracle_math_selftest(_p(x, ctypes.c_double), _p(y, ctypes.c_double), len(x),
+                               _p(out, ctypes.c_double))
+    return out
+
+
+def philox(ctr, key):
+    out = (ctypes.c_uint32 * 4)()
+    lib().oracle_philox(*[int(c) & 0xFFFFFFFF for c in ctr], *[int(k) & 0xFFFFFFFF for k in key],
+                        out)
+    return [int(v) for v in out]

@@ -1,0 +1,73 @@
+"""Map reference snapshots (tests/golden/episodes.npz) onto the SoA state."""
+import os
+
+import numpy as np
+
+from grasp_lab_salp_amd._abi import FIELD, NUM_FIELDS, MAX_OBSTACLES
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+VEC_MAP = {"v": "velocity", "w": "angular_velocity", "acc": "acceleration",
+           "alpha": "angular_acceleration", "eta": "euler_angle", "pw": "position_world",
+           "pos": "position", "ang": "angle", "ppos": "prev_position", "pang": "prev_angle",
+           "avgv": "avg_cycle_velocity", "avgw": "avg_cycle_angular_velocity"}
+SCAL_MAP = {"length": "r_length", "width": "r_width", "volume": "r_volume",
+            "prev_volume": "r_prev_water_volume", "cycle_time": "r_cycle_time",
+            "time": "r_time", "refill_time": "r_refill_time", "jet_time": "r_jet_time",
+            "coast_time": "r_coast_time", "contraction": "r_contraction",
+            "contract_rate": "r__contract_rate", "release_rate": "r__release_rate",
+            "phase": "r_phase", "cycle": "r_cycle", "angle1": "n_angle1", "angle2": "n_angle2",
+            "yaw": "n_yaw", "prev_yaw": "n_prev_yaw", "turn_time": "n_turn_time",
+            "n_obst": "e_n_obstacles", "prev_dist": "e_prev_dist", "ep_len": "e_ep_len",
+            "path_len": "e_path_length", "sum_a0": "e_sum_a0",
+            "sum_a1": "e_sum_a1", "sum_abs_a2": "e_sum_abs_a2", "sum_vel": "e_sum_vel",
+            "init_dist": "e_initial_distance"}
+
+# fields of the minimal state that a reference snapshot determines
+COMPARED = ([f"{k}{i}" for k in VEC_MAP for i in range(3)]
+            + list(SCAL_MAP) + ["com", "com_rate", "com_acc"] + [f"prev_I{i}" for i in range(3)]
+            + ["target0", "target1"] + [f"obst{i}" for i in range(2 * MAX_OBSTACLES)]
+            + ["prev_a2", "last_px", "last_py", "geom32", "pvol32"] + [f"sum_r{i}" for i in range(7)])
+
+
+def load_episodes():
+    return dict(np.load(os.path.join(GOLDEN, "episodes.npz")))
+
+
+def load_trace():
+    return dict(np.load(os.path.join(GOLDEN, "tick_trace.npz")))
+
+
+def snapshot_to_state(d, prefix, rows):
+    """Columns of the SoA state for fixture rows `rows` using snapshot `prefix`
+    ('b_' before the step, 'a_' after it, 'r_' after the auto-reset)."""
+    rows = np.asarray(rows)
+    n = len(rows)
+    s = np.zeros((NUM_FIELDS, n), np.float64)
+    g = lambda k: d[prefix + k][rows]
+    for short, ref in VEC_MAP.items():
+        v = g("r_" + ref)
+        for i in range(3):
+            s[FIELD[f"{short}{i}"]] = v[:, i]
+    for short, ref in SCAL_MAP.items():
+        s[FIELD[short]] = g(ref)
+    s[FIELD["com"]] = g("r_center_of_mass")[:, 0]
+    s[FIELD["com_rate"]] = g("r_center_of_mass_rate")[:, 0]
+    s[FIELD["com_acc"]] = g("r_center_of_mass_acc_rate")[:, 0]
+    pI = g("r_prev_I")
+    for i in range(3):
+        s[FIELD[f"prev_I{i}"]] = pI[:, i]
+    s[FIELD["geom32"]] = g("r_len_is_f32")
+    s[FIELD["pvol32"]] = g("r_pvol_is_f32")
+    t = g("e_target")
+    s[FIELD["target0"]], s[FIELD["target1"]] = t[:, 0], t[:, 1]
+    ob = g("e_obstacles").reshape(n, -1)
+    for i in range(2 * MAX_OBSTACLES):
+        s[FIELD[f"obst{i}"]] = ob[:, i]
+    s[FIELD["prev_a2"]] = g("e_prev_action")[:, 2]
+    lp = g("e_last_pos")
+    s[FIELD["last_px"]], s[FIELD["last_py"]] = lp[:, 0], lp[:, 1]
+    sc = g("e_sum_comp")
+    for i in range(7):
+        s[FIELD[f"sum_r{i}"]] = sc[:, i]
+    return s
