@@ -1,0 +1,87 @@
+"""ctypes binding of libsalp.so (the HIP/gfx950 build of include/salp.h).
+
+The library is built in-tree (``python -m grasp_lab_salp_amd.build`` or
+``__graft_entry__.build()``) and loaded from this package directory.  There is
+no CPU fallback: if the library or a GPU is missing, :func:`lib` raises.
+"""
+import ctypes
+import os
+
+from ._abi import ABI_VERSION, FIELDS, NUM_FIELDS, SalpParams
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libsalp.so")
+
+_lib = None
+
+
+class SalpError(RuntimeError):
+    pass
+
+
+class SalpRolloutBuffers(ctypes.Structure):
+    _fields_ = [
+        ("capacity", ctypes.c_int64),
+        ("obs", ctypes.c_void_p),
+        ("actions", ctypes.c_void_p),
+        ("rewards", ctypes.c_void_p),
+        ("dones", ctypes.c_void_p),
+        ("steps_done", ctypes.c_void_p),
+        ("max_steps", ctypes.c_int64),
+    ]
+
+
+# name -> (restype, argtypes); exactly the functions declared in include/salp.h
+_V, _H = ctypes.c_void_p, ctypes.c_void_p
+SIGNATURES = {
+    "salp_abi_version": (ctypes.c_int, []),
+    "salp_default_params": (None, [ctypes.POINTER(SalpParams)]),
+    "salp_create": (ctypes.c_int, [ctypes.POINTER(SalpParams), ctypes.c_int64, ctypes.c_uint64,
+                                   ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "salp_destroy": (ctypes.c_int, [_H]),
+    "salp_last_error": (ctypes.c_char_p, [_H]),
+    "salp_num_envs": (ctypes.c_int64, [_H]),
+    "salp_obs_dim": (ctypes.c_int, [_H]),
+    "salp_reset": (ctypes.c_int, [_H, _V, _V, _V]),
+    "salp_reset_to": (ctypes.c_int, [_H, _V, _V, _V, _V, _V, _V]),
+    "salp_step": (ctypes.c_int, [_H, _V, _V, _V, _V, _V, ctypes.c_int, _V, _V, _V]),
+    "salp_rollout": (ctypes.c_int, [_H, ctypes.c_int64, ctypes.POINTER(SalpRolloutBuffers), _V]),
+    "salp_step_random": (ctypes.c_int, [_H, ctypes.c_int32, _V, _V]),
+    "salp_num_fields": (ctypes.c_int, []),
+    "salp_field_name": (ctypes.c_char_p, [ctypes.c_int]),
+    "salp_get_state": (ctypes.c_int, [_H, _V, _V]),
+    "salp_set_state": (ctypes.c_int, [_H, _V, _V]),
+    "salp_state_ptr": (ctypes.c_int64, [_H]),
+    "salp_math_selftest": (ctypes.c_int, [_V, _V, ctypes.c_int64, _V, _V]),
+}
+
+
+def load(path=LIB_PATH):
+    """Load and type the shared library (no GPU needed for loading)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise SalpError(f"{path} not found: build it with `python -m grasp_lab_salp_amd.build` "
+                        "(there is no CPU fallback for the simulator)")
+    L = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    if L.salp_abi_version() != ABI_VERSION:
+        raise SalpError("libsalp ABI version mismatch")
+    if L.salp_num_fields() != NUM_FIELDS:
+        raise SalpError("libsalp state layout does not match grasp_lab_salp_amd._abi")
+    for i, name in enumerate(FIELDS):
+        if L.salp_field_name(i).decode() != name:
+            raise SalpError(f"field {i}: library says {L.salp_field_name(i)!r}, _abi says {name!r}")
+    _lib = L
+    return L
+
+
+def check(rc, handle=None):
+    if rc != 0:
+        msg = load().salp_last_error(handle)
+        raise SalpError(f"libsalp error {rc}: {msg.decode() if msg else ''}")
+    return rc

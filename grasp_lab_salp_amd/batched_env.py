@@ -1,0 +1,213 @@
+"""BatchedSalpEnv — n SALP envs on one GPU, torch tensors in and out.
+
+This is the batched form of the reference's ``SalpRobotEnv``
+(src/salp_robot_env.py:22-670): every call runs the corresponding reference
+method for all envs at once in libsalp.so (HIP, gfx950).  Tensors are
+torch.cuda tensors on the handle's device; work is enqueued on torch's
+current stream and nothing synchronises unless a result is read on the host.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._abi import (EPISODE_METRIC_KEYS, FIELD, FIELDS, INFO, INFO_DIM, INFO_KEYS, MAX_OBSTACLES,
+                   NUM_FIELDS, REWARD_COMPONENT_KEYS, SalpParams, default_params)
+
+__all__ = ["BatchedSalpEnv", "StepResult"]
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class StepResult:
+    """Outputs of one batched env.step (all device tensors)."""
+
+    __slots__ = ("obs", "reward", "terminated", "truncated", "terminal_obs", "info")
+
+    def __init__(self, obs, reward, terminated, truncated, terminal_obs, info):
+        self.obs, self.reward = obs, reward
+        self.terminated, self.truncated = terminated, truncated
+        self.terminal_obs, self.info = terminal_obs, info
+
+    def __iter__(self):  # obs, reward, terminated, truncated, info — gymnasium order
+        return iter((self.obs, self.reward, self.terminated, self.truncated, self.info))
+
+
+class BatchedSalpEnv:
+    """``n_envs`` independent reference envs simulated in one kernel per call.
+
+    Args:
+        n_envs: number of envs on this device.
+        params: :class:`SalpParams` (constructor arguments of Nozzle / Robot /
+            SalpRobotEnv); defaults to the canonical ``make_env`` config of
+            src/train_robot.py:11-21.
+        seed: Philox key for synthetic actions and reset draws.
+        env_id_offset: global id of env 0 (multi-GPU sharding: trajectories of
+            a given global env id do not depend on the sharding).
+        device: CUDA (HIP) device index.
+    """
+
+    def __init__(self, n_envs, params=None, seed=0, env_id_offset=0, device=None):
+        if not torch.cuda.is_available():
+            raise _lib.SalpError("BatchedSalpEnv needs a ROCm GPU (no CPU fallback)")
+        L = _lib.load()
+        self.params = params if params is not None else default_params()
+        if not isinstance(self.params, SalpParams):
+            raise TypeError("params must be a SalpParams")
+        self.n_envs = int(n_envs)
+        self.seed = int(seed)
+        self.env_id_offset = int(env_id_offset)
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(L.salp_create(ctypes.byref(self.params), self.n_envs, self.seed,
+                                     self.env_id_offset, self.device.index, ctypes.byref(h)))
+        self._h = h
+        self.obs_dim = L.salp_obs_dim(h)
+        self.num_obstacles = self.params.num_obstacles
+        self._info = torch.zeros((self.n_envs, INFO_DIM), dtype=torch.float64, device=self.device)
+
+    # ------------------------------------------------------------ plumbing
+    @property
+    def handle(self):
+        return self._h
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _check(self, rc):
+        return _lib.check(rc, self._h)
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib.load().salp_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _f32(self, x, shape):
+        t = torch.as_tensor(x, dtype=torch.float32, device=self.device).reshape(shape).contiguous()
+        return t
+
+    def _mask(self, mask):
+        if mask is None:
+            return None
+        return torch.as_tensor(mask, device=self.device).reshape(self.n_envs).to(torch.uint8).contiguous()
+
+    # ------------------------------------------------------------- env API
+    def reset(self, mask=None):
+        """reset() of every env (or of the masked ones); returns obs [n, obs_dim].
+
+        Targets and obstacles come from the env's Philox stream (the reference
+        uses the process-global np.random, src/salp_robot_env.py:484-487)."""
+        obs = torch.zeros((self.n_envs, self.obs_dim), dtype=torch.float32, device=self.device)
+        m = self._mask(mask)
+        self._check(_lib.load().salp_reset(self._h, _ptr(m), _ptr(obs), self._stream()))
+        return obs
+
+    def reset_to(self, targets, obstacles, n_obstacles=None, mask=None):
+        """reset() with caller-given targets [n,2] and obstacles [n,k,2]."""
+        t = self._f32(targets, (self.n_envs, 2))
+        ob = torch.as_tensor(obstacles, dtype=torch.float32, device=self.device).reshape(self.n_envs, -1, 2)
+        o = torch.zeros((self.n_envs, MAX_OBSTACLES, 2), dtype=torch.float32, device=self.device)
+        o[:, :ob.shape[1]] = ob
+        if n_obstacles is None:
+            n_obstacles = torch.full((self.n_envs,), min(ob.shape[1], self.num_obstacles))
+        k = torch.as_tensor(n_obstacles, device=self.device).reshape(self.n_envs).to(torch.int32).contiguous()
+        obs = torch.zeros((self.n_envs, self.obs_dim), dtype=torch.float32, device=self.device)
+        m = self._mask(mask)
+        self._check(_lib.load().salp_reset_to(self._h, _ptr(m), _ptr(t), _ptr(o.contiguous()), _ptr(k),
+                                              _ptr(obs), self._stream()))
+        return obs
+
+    def step(self, actions, auto_reset=False, want_terminal_obs=True):
+        """One env.step per env. actions [n,3] float32 in Box([0,0,-1],[1,1,1]).
+
+        Returns a :class:`StepResult`; ``info`` is an [n, INFO_DIM] fp64 tensor
+        (columns ``_abi.INFO_KEYS``; see :meth:`info_dicts`)."""
+        a = self._f32(actions, (self.n_envs, 3))
+        obs = torch.empty((self.n_envs, self.obs_dim), dtype=torch.float32, device=self.device)
+        rew = torch.empty(self.n_envs, dtype=torch.float64, device=self.device)
+        term = torch.empty(self.n_envs, dtype=torch.uint8, device=self.device)
+        trunc = torch.empty(self.n_envs, dtype=torch.uint8, device=self.device)
+        tobs = (torch.empty((self.n_envs, self.obs_dim), dtype=torch.float32, device=self.device)
+                if want_terminal_obs else None)
+        info = torch.empty((self.n_envs, INFO_DIM), dtype=torch.float64, device=self.device)
+        self._check(_lib.load().salp_step(self._h, _ptr(a), _ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc),
+                                          int(bool(auto_reset)), _ptr(tobs), _ptr(info), self._stream()))
+        return StepResult(obs, rew, term.bool(), trunc.bool(), tobs, info)
+
+    def step_random(self, n_steps):
+        """n_steps synthetic random-action env-steps per env (lock-step, auto-reset).
+        Returns the per-env reward sum (fp64)."""
+        rs = torch.empty(self.n_envs, dtype=torch.float64, device=self.device)
+        self._check(_lib.load().salp_step_random(self._h, int(n_steps), _ptr(rs), self._stream()))
+        return rs
+
+    def rollout(self, tick_budget, buffers=None, steps_done=None, max_steps=0):
+        """Chained random-action rollout: each env runs ``tick_budget`` physics
+        ticks, completing as many env-steps as fit (auto-reset).  ``buffers`` is
+        an optional dict of preallocated device tensors {obs [cap,n,obs_dim],
+        actions [cap,n,3], rewards [cap,n] f32, dones [cap,n] u8}; ``steps_done``
+        an int64 [n] tensor updated in place."""
+        B = _lib.SalpRolloutBuffers()
+        cap = 0
+        if buffers:
+            for k in ("obs", "actions", "rewards", "dones"):
+                t = buffers.get(k)
+                if t is not None:
+                    if not t.is_contiguous() or t.device != self.device:
+                        raise ValueError(f"buffer {k} must be contiguous on {self.device}")
+                    if t.shape[1] != self.n_envs:
+                        raise ValueError(f"buffer {k} must be [capacity, n_envs, ...]")
+                    cap = t.shape[0] if cap == 0 else min(cap, t.shape[0])
+                    setattr(B, k, t.data_ptr())
+        B.capacity = cap
+        if steps_done is not None:
+            if steps_done.dtype != torch.int64 or steps_done.numel() != self.n_envs:
+                raise ValueError("steps_done must be an int64 tensor with n_envs elements")
+            B.steps_done = steps_done.data_ptr()
+        B.max_steps = int(max_steps)
+        self._check(_lib.load().salp_rollout(self._h, int(tick_budget), ctypes.byref(B), self._stream()))
+        return steps_done
+
+    # ------------------------------------------------------------ state
+    def get_state(self):
+        """[NUM_FIELDS, n] fp64 copy of the struct-of-arrays state."""
+        s = torch.empty((NUM_FIELDS, self.n_envs), dtype=torch.float64, device=self.device)
+        self._check(_lib.load().salp_get_state(self._h, _ptr(s), self._stream()))
+        return s
+
+    def set_state(self, state):
+        s = torch.as_tensor(state, dtype=torch.float64, device=self.device).reshape(NUM_FIELDS, self.n_envs)
+        s = s.contiguous()
+        self._check(_lib.load().salp_set_state(self._h, _ptr(s), self._stream()))
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def field(self, name):
+        return self.get_state()[FIELD[name]]
+
+    # ------------------------------------------------------------- info
+    @staticmethod
+    def info_dicts(info, dones=None):
+        """Build reference-style info dicts (src/salp_robot_env.py:279-289) on the
+        host — reward components always, episode metrics only where done."""
+        info = info.detach().cpu().numpy()
+        out = []
+        for row in info:
+            d = {k: float(row[INFO[k]]) for k in REWARD_COMPONENT_KEYS}
+            if row[INFO["has_metrics"]] != 0:
+                for k in EPISODE_METRIC_KEYS:
+                    d[k] = float(row[INFO[k]])
+            out.append(d)
+        return out
+
+
+FIELDS = FIELDS
+INFO_KEYS = INFO_KEYS

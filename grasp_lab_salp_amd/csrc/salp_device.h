@@ -1,0 +1,773 @@
+/*
+ * salp_device.h — per-lane SALP physics for gfx950 (one env per lane).
+ *
+ * Restates the reference hot path (Avielstein/GRASP_LAB_SALP src/robot.py,
+ * src/dynamics.py, src/geometry.py, src/salp_robot_env.py) for registers:
+ *
+ *  - Every 3x3 matrix the reference builds is diagonal, a rotation with known
+ *    zeros, or x-only (center of mass, jet moment arm).  The products below keep
+ *    the reference's (NumPy/OpenBLAS) evaluation order of every NON-zero term
+ *    and drop the terms that are exact zeros (x*0, x+0), so results equal the
+ *    full-matrix evaluation bit for bit (signed zeros aside).  The CPU oracle
+ *    (oracle/salp_oracle.c) evaluates the full matrices; tests compare the two
+ *    exactly.
+ *  - fp64 throughout (the reference is NumPy fp64); the few float32 operations
+ *    are the ones NumPy 2 performs in float32 (NEP 50: float32 action ->
+ *    contraction -> body geometry while REFILL runs past refill_time).
+ *  - Quantities that only depend on (length, width, volume, prev volume) are
+ *    recomputed at the start of each tick instead of being stored, which is
+ *    what Robot.update_properties computes one call earlier.
+ *
+ * Hot state lives in registers for the whole breathing cycle (~700 ticks);
+ * cold env state (targets, obstacles, episode trackers) is read/written in the
+ * struct-of-arrays state buffer only at env-step boundaries.
+ */
+#ifndef SALP_DEVICE_H
+#define SALP_DEVICE_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/salp.h"
+#include "salp_math.h"
+#include "salp_philox.h"
+
+#pragma clang fp contract(off)
+
+#define SD static __device__ __forceinline__
+
+namespace salp {
+
+constexpr double DT = 0.01;                                /* src/robot.py:293 */
+constexpr double PI = 3.141592653589793;
+constexpr double COS_GAMMA = 0x1.6a09e667f3bcdp-1;         /* np.cos(np.pi/4) */
+constexpr double SIN_GAMMA = 0x1.6a09e667f3bccp-1;         /* np.sin(np.pi/4) */
+constexpr double REFILL_C0 = -0x1.f3ffffffffffcp+8, REFILL_C1 = 0x1.5bffffffffffcp+6,
+                 REFILL_C2 = -0x1.ccccccccccccbp-2;       /* np.polyfit, src/geometry.py:6-10 */
+constexpr double PROPUL_C0 = -0x1.f400000000001p+7, PROPUL_C1 = 0x1.97ffffffffffep+4,
+                 PROPUL_C2 = -0x1.0000000000003p-3;       /* src/geometry.py:18-22 */
+constexpr double BUOY_MASS = 0.195, SKIN_MASS = 0.145, TUBE_MASS = 0.414; /* src/robot.py:286-288 */
+constexpr double CD = 0.3, DRAG_FORCE_RATIO = 0.25, DRAG_TORQUE_RATIO = 0.1; /* :300-302 */
+constexpr double AMF0 = 0.5, AMF1 = 0.6, AMF2 = 0.6, AMRF = 0.2;  /* :303-304 */
+constexpr double AMT0 = 0.3, AMT1 = 0.6, AMT2 = 0.6;              /* :305 */
+enum { REFILL = 0, JET = 1, COAST = 2, REST = 3 };
+
+/* Launch-invariant constants derived on the host from SalpParams (kernel arg,
+ * read through the scalar cache). */
+struct Params {
+    double L0, W0, maxc, dry_mass, nozzle_mass, density, nozzle_area;
+    double mid_x;            /* nozzle middle position x = -(length1 + length2) */
+    double tube_volume;      /* src/robot.py:295 */
+    double tube_volume_I;    /* src/geometry.py:140 (different pi literal) */
+    double net_tube_mass;    /* src/geometry.py:157 */
+    double com_mass_sum;     /* tube + nozzle + buoy + skin masses */
+    double P1000tv;          /* 1000 * tube_volume (src/geometry.py:198) */
+    double init_aspect, end_aspect, aspect_den;
+    double angle_speed;      /* 31*pi/30 */
+    double obstacle_radius, x_min, x_max, y_min, y_max, sep;
+    double init_angle1, init_angle2;
+    int32_t num_obstacles, max_cycles, obs_dim;
+    int64_t n;               /* envs on this device (SoA stride) */
+    int64_t env_offset;      /* global id of env 0 */
+    uint64_t seed;
+};
+
+/* ----------------------------------------------------------- helpers */
+SD double pymax(double a, double b) { return b > a ? b : a; }
+SD float sqf(float x) { return (float)((double)x * (double)x); }
+SD float cubef(float x) {
+    double p = (double)x * (double)x;
+    double h = p * (double)x, e = sm_fma(p, (double)x, -h);
+    float r = (float)h;
+    double d = h - (double)r;
+    float nb = nextafterf(r, d > 0 ? INFINITY : -INFINITY);
+    double ulp = (double)nb - (double)r;
+    if (d != 0.0 && fabs(d) * 2.0 == fabs(ulp) && e != 0.0) r = ((e > 0) == (d > 0)) ? nb : r;
+    return r;
+}
+
+/* Rotation R = Rz(psi) Ry(theta) Rx(phi) (src/dynamics.py:34-58) from the
+ * dgemm-order product with its zeros removed. */
+struct Rot { double r[3][3]; };
+SD Rot rot_zyx(double phi, double theta, double psi) {
+    double sp, cp, st, ct, ss, cs;
+    sm_sincos(phi, &sp, &cp);
+    sm_sincos(theta, &st, &ct);
+    sm_sincos(psi, &ss, &cs);
+    /* A = Rz @ Ry */
+    double a00 = cs * ct, a01 = -ss, a02 = cs * st;
+    double a10 = ss * ct, a11 = cs, a12 = ss * st;
+    double a20 = -st, a22 = ct;
+    Rot R;
+    R.r[0][0] = a00; R.r[0][1] = sm_fma(a02, sp, a01 * cp); R.r[0][2] = sm_fma(a02, cp, a01 * -sp);
+    R.r[1][0] = a10; R.r[1][1] = sm_fma(a12, sp, a11 * cp); R.r[1][2] = sm_fma(a12, cp, a11 * -sp);
+    R.r[2][0] = a20; R.r[2][1] = a22 * sp;                   R.r[2][2] = a22 * cp;
+    return R;
+}
+/* R @ v (dgemv order) */
+SD void rot_apply(const Rot& R, double v0, double v1, double v2, double* o) {
+    for (int i = 0; i < 3; ++i) o[i] = sm_fma(R.r[i][2], v2, sm_fma(R.r[i][0], v0, R.r[i][1] * v1));
+}
+/* R.T @ (d0, d1, 0) (transposed view order), components 0 and 1 */
+SD void rot_body_xy(const Rot& R, double d0, double d1, double* b0, double* b1) {
+    *b0 = sm_fma(R.r[1][0], d1, R.r[0][0] * d0);
+    *b1 = sm_fma(R.r[1][1], d1, R.r[0][1] * d0);
+}
+
+/* ---------------------------------------------- geometry (src/geometry.py) */
+/* body geometry derived from (length, width, volume, prev volume) */
+struct Geo {
+    double A0, A1;           /* cross-sectional areas yz, xz(=xy) */
+    double wm, m, mr;        /* water mass, total mass, mass rate */
+    double nr;               /* drag-coefficient interpolation ratio (clipped) */
+    double I0, I1;           /* inertia diag xx, yy(=zz) */
+};
+
+/* compute_water_volume_jit (src/geometry.py:78-81) */
+SD double ellipsoid_volume(double L, double W, bool f32) {
+    if (f32) {
+        float lh = (float)L / 2.0f, wh = (float)W / 2.0f;
+        return (double)((float)((4.0 / 3.0) * PI) * lh * sqf(wh));
+    }
+    double wh = W / 2.0;
+    return (4.0 / 3.0) * PI * (L / 2.0) * (wh * wh);
+}
+/* Robot._get_water_volume (src/robot.py:1055-1056) */
+SD double water_volume(const Params& P, double L, double W, bool f32) {
+    if (f32) return (double)((float)ellipsoid_volume(L, W, true) - (float)P.tube_volume);
+    return ellipsoid_volume(L, W, false) - P.tube_volume;
+}
+/* water mass = density * volume (src/robot.py:1058-1063) */
+SD double water_mass(const Params& P, double V, bool f32) {
+    return f32 ? (double)((float)P.density * (float)V) : P.density * V;
+}
+
+SD Geo geometry(const Params& P, double L, double W, double V, double pV, bool g32, bool pv32) {
+    Geo g;
+    /* compute_cross_sectional_area_jit (src/geometry.py:67-75) */
+    if (g32) {
+        float wh = (float)W / 2.0f, lh = (float)L / 2.0f, pi = (float)PI;
+        g.A0 = (double)(pi * wh * wh);
+        g.A1 = (double)(pi * lh * wh);
+    } else {
+        double wh = W / 2.0, lh = L / 2.0;
+        g.A0 = PI * wh * wh;
+        g.A1 = PI * lh * wh;
+    }
+    /* get_mass / get_mass_rate (src/robot.py:1061-1066, 651-654) */
+    g.wm = water_mass(P, V, g32);
+    double pwm = pv32 ? (double)((float)pV * (float)P.density) : pV * P.density;
+    if (g32) {
+        g.m = (double)((float)P.dry_mass + (float)g.wm + (float)P.nozzle_mass);
+    } else {
+        g.m = P.dry_mass + g.wm + P.nozzle_mass;
+    }
+    if (g32 && pv32) g.mr = (double)(((float)g.wm - (float)pwm) / (float)DT);
+    else g.mr = (g.wm - pwm) / DT;
+    /* compute_drag_coefficient_jit (src/geometry.py:104-123) */
+    double nr;
+    if (g32) {
+        float aspect = (float)L / (float)W;
+        nr = (double)((aspect - (float)P.end_aspect) / (float)P.aspect_den);
+    } else {
+        nr = (L / W - P.end_aspect) / P.aspect_den;
+    }
+    if (nr < 0.0) nr = 0.0;
+    if (nr > 1.0) nr = 1.0;
+    g.nr = nr;
+    /* compute_inertia_matrix_jit (src/geometry.py:133-183) */
+    if (g32) {
+        float lh = (float)L / 2.0f, wh = (float)W / 2.0f;
+        float lh2 = sqf(lh), wh2 = sqf(wh);
+        float t8 = sqf(lh - 0.08f), n25 = sqf(lh + 0.025f);
+        float p1 = (float)(1.0 / 3.0 * SKIN_MASS);
+        float k = 0.2f * (1000.0f * (float)ellipsoid_volume(L, W, true));
+        float sxx = p1 * (wh2 + wh2), syy = p1 * (lh2 + wh2);
+        float wxx = k * (wh2 + wh2), wyy = k * (lh2 + wh2);
+        g.I0 = (double)sxx + (double)wxx;
+        g.I1 = BUOY_MASS * (double)lh2 + P.net_tube_mass * (double)t8 + (double)syy + (double)wyy +
+               P.nozzle_mass * (double)n25;
+    } else {
+        double lh = L / 2.0, wh = W / 2.0;
+        double lh2 = lh * lh, wh2 = wh * wh;
+        double t8 = lh - 0.08, n25 = lh + 0.025;
+        double p1 = 1.0 / 3.0 * SKIN_MASS;
+        double k = 0.2 * (1000.0 * ellipsoid_volume(L, W, false));
+        g.I0 = p1 * (wh2 + wh2) + k * (wh2 + wh2);
+        g.I1 = BUOY_MASS * lh2 + P.net_tube_mass * (t8 * t8) + p1 * (lh2 + wh2) + k * (lh2 + wh2) +
+               P.nozzle_mass * (n25 * n25);
+    }
+    return g;
+}
+
+/* compute_center_of_mass_jit (src/geometry.py:186-203), x component */
+SD double center_of_mass(const Params& P, double L, double W, double wm, bool f32) {
+    if (f32) {
+        float Lf = (float)L;
+        float pbx = Lf / 2.0f, ptx = Lf / 2.0f - 0.08f, pnx = -Lf / 2.0f - 0.025f + 0.05f;
+        float wme = 1000.0f * (float)ellipsoid_volume(L, W, true);
+        double num = (double)wme * 0.0 - P.P1000tv * (double)ptx;
+        float den = wme - (float)P.P1000tv;
+        double pwx = num / (double)den;
+        float total = (float)P.com_mass_sum + (float)wm;
+        return (TUBE_MASS * (double)ptx + P.nozzle_mass * (double)pnx + BUOY_MASS * (double)pbx +
+                SKIN_MASS * 0.0 + wm * pwx) / (double)total;
+    }
+    double pbx = L / 2, ptx = L / 2 - 0.08, pnx = -L / 2 - 0.025 + 0.05;
+    double wme = 1000.0 * ellipsoid_volume(L, W, false);
+    double pwx = (wme * 0.0 - P.P1000tv * ptx) / (wme - P.P1000tv);
+    double total = P.com_mass_sum + wm;
+    return (TUBE_MASS * ptx + P.nozzle_mass * pnx + BUOY_MASS * pbx + SKIN_MASS * 0.0 + wm * pwx) /
+           total;
+}
+
+/* compute_length_jit / compute_width_jit (src/geometry.py:39-64) */
+SD double body_length(const Params& P, int st, double ct, double refill, double mx, double c,
+                      double cr, double rr, bool* f32) {
+    *f32 = false;
+    if (st == REFILL) {
+        if (ct < refill) return P.L0 - ct * cr;
+        *f32 = true;
+        return (double)((float)P.L0 - (float)c);
+    }
+    if (st == JET) return (double)((float)P.L0 - (float)c) + (ct - mx) * rr;
+    return P.L0;
+}
+SD double body_width(const Params& P, int st, double ct, double refill, double mx, double c,
+                     double cr, double rr) {
+    if (st == REFILL) {
+        if (ct < refill) return P.W0 + ct * cr;
+        return (double)((float)P.W0 + (float)c);
+    }
+    if (st == JET) return (double)((float)P.W0 + (float)c) - (ct - mx) * rr;
+    return P.W0;
+}
+
+/* ---------------------------------------------------- per-lane state */
+struct Hot {
+    double v0, v1, v2, w0, w1, w2, a0, a1, a2, al0, al1, al2;   /* vel, ang vel, acc, ang acc */
+    double e0, e1, e2, p0, p1, p2, q0, q1, q2, g0, g1, g2;        /* euler, pos world, position, angle */
+    double L, W, V, pV, com, comr, coma, pI0, pI1, pI2;
+    double ct, time;
+    double refill, jet, coast, c, cr, rr, turn;                /* cycle constants */
+    double mx, b1, b2;                                         /* phase boundaries */
+    double d0, d1, d2;                                         /* nozzle direction */
+    int phase;
+    bool g32, pv32;
+};
+
+#define SF(f) S[(size_t)(f) * (size_t)P.n + (size_t)i]
+
+SD void load_hot(Hot& h, const double* S, const Params& P, int64_t i) {
+    h.v0 = SF(SALP_F_V0); h.v1 = SF(SALP_F_V1); h.v2 = SF(SALP_F_V2);
+    h.w0 = SF(SALP_F_W0); h.w1 = SF(SALP_F_W1); h.w2 = SF(SALP_F_W2);
+    h.a0 = SF(SALP_F_ACC0); h.a1 = SF(SALP_F_ACC1); h.a2 = SF(SALP_F_ACC2);
+    h.al0 = SF(SALP_F_ALPHA0); h.al1 = SF(SALP_F_ALPHA1); h.al2 = SF(SALP_F_ALPHA2);
+    h.e0 = SF(SALP_F_ETA0); h.e1 = SF(SALP_F_ETA1); h.e2 = SF(SALP_F_ETA2);
+    h.p0 = SF(SALP_F_PW0); h.p1 = SF(SALP_F_PW1); h.p2 = SF(SALP_F_PW2);
+    h.q0 = SF(SALP_F_POS0); h.q1 = SF(SALP_F_POS1); h.q2 = SF(SALP_F_POS2);
+    h.g0 = SF(SALP_F_ANG0); h.g1 = SF(SALP_F_ANG1); h.g2 = SF(SALP_F_ANG2);
+    h.L = SF(SALP_F_LENGTH); h.W = SF(SALP_F_WIDTH); h.V = SF(SALP_F_VOLUME);
+    h.pV = SF(SALP_F_PREV_VOLUME); h.com = SF(SALP_F_COM); h.comr = SF(SALP_F_COM_RATE);
+    h.coma = SF(SALP_F_COM_ACC);
+    h.pI0 = SF(SALP_F_PREV_I0); h.pI1 = SF(SALP_F_PREV_I1); h.pI2 = SF(SALP_F_PREV_I2);
+    h.g32 = SF(SALP_F_GEOM32) != 0.0; h.pv32 = SF(SALP_F_PVOL32) != 0.0;
+    h.ct = SF(SALP_F_CYCLE_TIME); h.time = SF(SALP_F_TIME);
+    h.refill = SF(SALP_F_REFILL_TIME); h.jet = SF(SALP_F_JET_TIME); h.coast = SF(SALP_F_COAST_TIME);
+    h.c = SF(SALP_F_CONTRACTION); h.cr = SF(SALP_F_CONTRACT_RATE); h.rr = SF(SALP_F_RELEASE_RATE);
+    h.turn = SF(SALP_F_TURN_TIME);
+    h.phase = (int)SF(SALP_F_PHASE);
+}
+SD void store_hot(const Hot& h, double* S, const Params& P, int64_t i) {
+    SF(SALP_F_V0) = h.v0; SF(SALP_F_V1) = h.v1; SF(SALP_F_V2) = h.v2;
+    SF(SALP_F_W0) = h.w0; SF(SALP_F_W1) = h.w1; SF(SALP_F_W2) = h.w2;
+    SF(SALP_F_ACC0) = h.a0; SF(SALP_F_ACC1) = h.a1; SF(SALP_F_ACC2) = h.a2;
+    SF(SALP_F_ALPHA0) = h.al0; SF(SALP_F_ALPHA1) = h.al1; SF(SALP_F_ALPHA2) = h.al2;
+    SF(SALP_F_ETA0) = h.e0; SF(SALP_F_ETA1) = h.e1; SF(SALP_F_ETA2) = h.e2;
+    SF(SALP_F_PW0) = h.p0; SF(SALP_F_PW1) = h.p1; SF(SALP_F_PW2) = h.p2;
+    SF(SALP_F_POS0) = h.q0; SF(SALP_F_POS1) = h.q1; SF(SALP_F_POS2) = h.q2;
+    SF(SALP_F_ANG0) = h.g0; SF(SALP_F_ANG1) = h.g1; SF(SALP_F_ANG2) = h.g2;
+    SF(SALP_F_LENGTH) = h.L; SF(SALP_F_WIDTH) = h.W; SF(SALP_F_VOLUME) = h.V;
+    SF(SALP_F_PREV_VOLUME) = h.pV; SF(SALP_F_COM) = h.com; SF(SALP_F_COM_RATE) = h.comr;
+    SF(SALP_F_COM_ACC) = h.coma;
+    SF(SALP_F_PREV_I0) = h.pI0; SF(SALP_F_PREV_I1) = h.pI1; SF(SALP_F_PREV_I2) = h.pI2;
+    SF(SALP_F_GEOM32) = h.g32 ? 1.0 : 0.0; SF(SALP_F_PVOL32) = h.pv32 ? 1.0 : 0.0;
+    SF(SALP_F_CYCLE_TIME) = h.ct; SF(SALP_F_TIME) = h.time;
+    SF(SALP_F_REFILL_TIME) = h.refill; SF(SALP_F_JET_TIME) = h.jet; SF(SALP_F_COAST_TIME) = h.coast;
+    SF(SALP_F_CONTRACTION) = h.c; SF(SALP_F_CONTRACT_RATE) = h.cr; SF(SALP_F_RELEASE_RATE) = h.rr;
+    SF(SALP_F_TURN_TIME) = h.turn;
+    SF(SALP_F_PHASE) = (double)h.phase;
+}
+
+/* Nozzle.get_nozzle_direction (src/robot.py:138-150): R_br @ R_mb @ R_nm @
+ * [cos g, 0, sin g] with the matrices of _get_rotation_matrices (:187-208). */
+SD void nozzle_direction(double angle1, double angle2, double* d) {
+    const double cg = COS_GAMMA, sg = SIN_GAMMA;
+    double s1, c1, s2, c2;
+    sm_sincos(angle1, &s1, &c1);
+    sm_sincos(angle2, &s2, &c2);
+    /* R_nm = R_theta_fixed @ R_nozzle: columns 0 and 2 are all that is used */
+    double n00 = cg * c2, n10 = s2, n20 = sg * c2;
+    double n02 = -sg, n12 = 0.0, n22 = cg;
+    /* C = (R_br @ R_mb) @ R_nm ; rows of R_br@R_mb: (-0,-0,-1), (s1,c1,0), (c1,-s1,0) */
+    double c00 = -n20, c02 = -n22;
+    double c10 = sm_fma(c1, n10, s1 * n00), c12 = sm_fma(c1, n12, s1 * n02);
+    double c20 = sm_fma(-s1, n10, c1 * n00), c22 = sm_fma(-s1, n12, c1 * n02);
+    d[0] = sm_fma(c02, sg, c00 * cg);
+    d[1] = sm_fma(c12, sg, c10 * cg);
+    d[2] = sm_fma(c22, sg, c20 * cg);
+}
+/* phase boundaries of update_state / step_through_cycle (src/robot.py:640-649, 742) */
+SD void cycle_bounds(Hot& h) {
+    h.mx = pymax(h.refill, h.turn);
+    h.b1 = h.mx + h.jet;
+    h.b2 = h.b1 + h.coast;
+}
+
+/* --------------------------------------------------- one physics tick */
+/* Robot.step (src/robot.py:670-678): update_dynamics (:854-858) with
+ * _newton_equations (:789-823), _euler_equations (:825-851),
+ * _update_motion_states (:860-875); then cycle_time, update_state,
+ * update_properties (:640-668). */
+SD void tick(Hot& h, const Params& P) {
+    const Geo g = geometry(P, h.L, h.W, h.V, h.pV, h.g32, h.pv32);
+    const double m = g.m;
+    const double k = -0.5 * P.density;
+    /* ---------------- Newton ---------------- */
+    /* Coriolis force -w x (M v)  (src/dynamics.py:159-162) */
+    double mv0 = m * h.v0, mv1 = m * h.v1, mv2 = m * h.v2;
+    double cf0 = -(h.w1 * mv2 - h.w2 * mv1), cf1 = -(h.w2 * mv0 - h.w0 * mv2),
+           cf2 = -(h.w0 * mv1 - h.w1 * mv0);
+    /* drag force (src/dynamics.py:110-116) */
+    double vn = np_norm3(h.v0, h.v1, h.v2);
+    double tcd0 = 2.5 - g.nr * (2.5 - 1.5), tcd1 = 1.5 - g.nr * (1.5 - 2.5);
+    double ka0, ka1;
+    if (h.g32) { ka0 = (double)((float)k * (float)g.A0); ka1 = (double)((float)k * (float)g.A1); }
+    else { ka0 = g.A0 * k; ka1 = g.A1 * k; }
+    double kc0 = ka0 * tcd0, kc1 = ka1 * tcd1;
+    double df0 = kc0 * vn * h.v0 + kc0 * h.v0 * DRAG_FORCE_RATIO;
+    double df1 = kc1 * vn * h.v1 + kc1 * h.v1 * DRAG_FORCE_RATIO;
+    double df2 = kc1 * vn * h.v2 + kc1 * h.v2 * DRAG_FORCE_RATIO;
+    /* jet force (src/robot.py:937-951, src/dynamics.py:87-101) */
+    double jf0 = 0.0, jf1 = 0.0, jf2 = 0.0;
+    if (h.phase == JET) {
+        double speed;
+        if (h.g32 && h.pv32) {
+            float vr = ((float)h.V - (float)h.pV) / (float)DT;
+            speed = (double)(vr / (float)P.nozzle_area);
+        } else {
+            speed = ((h.V - h.pV) / DT) / P.nozzle_area;
+        }
+        jf0 = g.mr * (h.d0 * speed) * -CD;
+        jf1 = g.mr * (h.d1 * speed) * -CD;
+        jf2 = g.mr * (h.d2 * speed) * -CD;
+    }
+    /* added-mass force (src/dynamics.py:131-141) */
+    double am0 = m * AMF0, am1 = m * AMF1, am2 = m * AMF2, amr = g.mr * AMRF;
+    double amv0 = am0 * h.v0, amv1 = am1 * h.v1, amv2 = am2 * h.v2;
+    double af0 = -((am0 * h.a0 + (h.w1 * amv2 - h.w2 * amv1)) + amr * h.v0);
+    double af1 = -((am1 * h.a1 + (h.w2 * amv0 - h.w0 * amv2)) + amr * h.v1);
+    double af2 = -((am2 * h.a2 + (h.w0 * amv1 - h.w1 * amv0)) + amr * h.v2);
+    /* fictitious forces of the moving center of mass (src/robot.py:806-810);
+     * com = (cx, 0, 0) */
+    const double cx = h.com, crx = h.comr;
+    double acc_y = (h.w0 * (h.w1 * cx) + (h.w2 * crx) * 2.0) + h.al2 * cx;
+    double acc_z = (h.w0 * (h.w2 * cx) + -(h.w1 * crx) * 2.0) + -(h.al1 * cx);
+    double acc_x = (h.w1 * -(h.w1 * cx) - h.w2 * (h.w2 * cx)) + h.coma;
+    double ff0 = acc_x * m, ff1 = acc_y * m, ff2 = acc_z * m;
+    /* total force and linear acceleration (src/dynamics.py:5-10) */
+    double na0 = ((((jf0 + df0) + af0) + cf0) + ff0) / m;
+    double na1 = ((((jf1 + df1) + af1) + cf1) + ff1) / m;
+    double na2 = ((((jf2 + df2) + af2) + cf2) + ff2) / m;
+    /* ---------------- Euler ---------------- */
+    const double I0 = g.I0, I1 = g.I1;
+    /* Coriolis torque -w x (I w) (src/dynamics.py:165-168) */
+    double iw0 = I0 * h.w0, iw1 = I1 * h.w1, iw2 = I1 * h.w2;
+    double ct0 = -(h.w1 * iw2 - h.w2 * iw1), ct1 = -(h.w2 * iw0 - h.w0 * iw2),
+           ct2 = -(h.w0 * iw1 - h.w1 * iw0);
+    /* drag torque (src/dynamics.py:119-128) */
+    double wn = np_norm3(h.w0, h.w1, h.w2);
+    double dimx, dimy;
+    if (h.g32) { dimx = (double)cubef((float)h.W); dimy = (double)cubef((float)h.L); }
+    else { dimx = sm_cube(h.W); dimy = sm_cube(h.L); }
+    double rcd0 = 0.3 - g.nr * (0.3 - 0.1), rcd1 = 0.2 - g.nr * (0.2 - 0.5);
+    double ra0 = rcd0 * k * g.A0, ra1 = rcd1 * k * g.A1;
+    double dt0 = ra0 * wn * h.w0 * dimx + ra0 * h.w0 * h.W * DRAG_TORQUE_RATIO;
+    double dt1 = ra1 * wn * h.w1 * dimy + ra1 * h.w1 * h.W * DRAG_TORQUE_RATIO;
+    double dt2 = ra1 * wn * h.w2 * dimy + ra1 * h.w2 * h.W * DRAG_TORQUE_RATIO;
+    /* jet torque r x F, r = (mid_x - L/2, 0, 0) (src/robot.py:931-935) */
+    double rx = P.mid_x + -h.L / 2.0;
+    double jt1 = -(rx * jf2), jt2 = rx * jf1;
+    /* deformation torque -(dI/dt) w; prev_I <- I (src/robot.py:888-896) */
+    double ir0 = (I0 - h.pI0) / DT, ir1 = (I1 - h.pI1) / DT, ir2 = (I1 - h.pI2) / DT;
+    double dft0 = -(ir0 * h.w0), dft1 = -(ir1 * h.w1), dft2 = -(ir2 * h.w2);
+    h.pI0 = I0; h.pI1 = I1; h.pI2 = I1;
+    /* added-mass torque, I_rate term identically zero (src/dynamics.py:144-156) */
+    double at0 = I0 * AMT0, at1 = I1 * AMT1, at2 = I1 * AMT2;
+    double atw0 = at0 * h.w0, atw1 = at1 * h.w1, atw2 = at2 * h.w2;
+    double amt0 = -((at0 * h.al0 + (h.w1 * atw2 - h.w2 * atw1)) + (h.v1 * amv2 - h.v2 * amv1));
+    double amt1 = -((at1 * h.al1 + (h.w2 * atw0 - h.w0 * atw2)) + (h.v2 * amv0 - h.v0 * amv2));
+    double amt2 = -((at2 * h.al2 + (h.w0 * atw1 - h.w1 * atw0)) + (h.v0 * amv1 - h.v1 * amv0));
+    /* total torque and angular acceleration (src/dynamics.py:13-17) */
+    double nal0 = (((dt0 + ct0) + dft0) + amt0) / I0;
+    double nal1 = ((((jt1 + dt1) + ct1) + dft1) + amt1) / I1;
+    double nal2 = ((((jt2 + dt2) + ct2) + dft2) + amt2) / I1;
+    h.a0 = na0; h.a1 = na1; h.a2 = na2;
+    h.al0 = nal0; h.al1 = nal1; h.al2 = nal2;
+    /* ---------------- integrate (semi-implicit Euler) ---------------- */
+    h.v0 = h.v0 + na0 * DT; h.v1 = h.v1 + na1 * DT; h.v2 = h.v2 + na2 * DT;
+    h.w0 = h.w0 + nal0 * DT; h.w1 = h.w1 + nal1 * DT; h.w2 = h.w2 + nal2 * DT;
+    {   /* to_euler_angle_rate_jit (src/dynamics.py:20-31) */
+        double sp, cp, st, ctt;
+        sm_sincos(h.e0, &sp, &cp);
+        sm_sincos(h.e1, &st, &ctt);
+        double tt = st / ctt;
+        double r0 = sm_fma(cp * tt, h.w2, h.w0 + (sp * tt) * h.w1);
+        double r1 = sm_fma(-sp, h.w2, cp * h.w1);
+        double r2 = sm_fma(cp / ctt, h.w2, (sp / ctt) * h.w1);
+        h.e0 = h.e0 + r0 * DT; h.e1 = h.e1 + r1 * DT; h.e2 = h.e2 + r2 * DT;
+    }
+    {   /* to_world_frame_jit (src/dynamics.py:34-58) */
+        Rot R = rot_zyx(h.e0, h.e1, h.e2);
+        double vw[3];
+        rot_apply(R, h.v0, h.v1, h.v2, vw);
+        h.p0 = h.p0 + vw[0] * DT; h.p1 = h.p1 + vw[1] * DT; h.p2 = h.p2 + vw[2] * DT;
+    }
+    h.q0 = h.q0 + h.v0 * DT; h.q1 = h.q1 + h.v1 * DT; h.q2 = h.q2 + h.v2 * DT;
+    h.g0 = h.g0 + h.w0 * DT; h.g1 = h.g1 + h.w1 * DT; h.g2 = h.g2 + h.w2 * DT;
+    /* ---------------- clocks, phase, properties ---------------- */
+    h.ct += DT;
+    h.time += DT;
+    h.phase = h.ct <= h.mx ? REFILL : (h.ct <= h.b1 ? JET : (h.ct <= h.b2 ? COAST : REST));
+    h.pV = h.V;
+    h.pv32 = h.g32;
+    bool f32;
+    h.L = body_length(P, h.phase, h.ct, h.refill, h.mx, h.c, h.cr, h.rr, &f32);
+    h.W = body_width(P, h.phase, h.ct, h.refill, h.mx, h.c, h.cr, h.rr);
+    h.g32 = f32;
+    h.V = water_volume(P, h.L, h.W, f32);
+    double com = center_of_mass(P, h.L, h.W, water_mass(P, h.V, f32), f32);
+    double comr = (com - h.com) / DT;
+    h.coma = (comr - h.comr) / DT;
+    h.com = com;
+    h.comr = comr;
+}
+
+/* ------------------------------------------------ env-step prologue */
+/* SalpRobotEnv.step up to step_through_cycle's loop (src/salp_robot_env.py:
+ * 196-210; src/robot.py:62-98 IK, :544-592 set_control, :740-748). */
+SD void begin_step(Hot& h, double* S, const Params& P, int64_t i, float a0, float a1, float a2) {
+    SF(SALP_F_ACT0) = a0; SF(SALP_F_ACT1) = a1; SF(SALP_F_ACT2) = a2;
+    /* _rescale_action in float32 (src/salp_robot_env.py:166-174) */
+    float r0 = a0 * 0.06f, r1 = a1 * 10.0f, r2 = a2 * (float)(PI / 2);
+    /* Nozzle.set_yaw_angle + solve_angles */
+    SF(SALP_F_PREV_YAW) = SF(SALP_F_YAW);
+    SF(SALP_F_YAW) = (double)r2;
+    double pa1 = SF(SALP_F_ANGLE1), pa2 = SF(SALP_F_ANGLE2);
+    float sy, cy;
+    sm_np_sincosf(r2, &sy, &cy);
+    double t1 = -(double)sy, t2 = (double)cy;        /* R_br^T @ -[cos, sin, 0] */
+    double val2 = 2.0 * t2 - 1.0;
+    if (val2 < -1.0) val2 = -1.0;
+    if (val2 > 1.0) val2 = 1.0;
+    double an2 = sm_acos(val2), an1;
+    if (an2 <= -PI) an2 += 2 * PI;
+    else if (an2 > PI) an2 -= 2 * PI;
+    if (an2 == 0.0) {
+        an1 = 0.0;
+    } else {
+        double s2, c2;
+        sm_sincos(an2, &s2, &c2);
+        double a = 0.5 * (c2 - 1.0);
+        double b = sqrt(2.0) * s2 / 2.0;
+        double val1 = t1 / sqrt(a * a + b * b);
+        if (val1 < -1.0) val1 = -1.0;
+        if (val1 > 1.0) val1 = 1.0;
+        an1 = sm_asin(val1) - sm_atan2(b, a);
+    }
+    if (an1 <= -PI) an1 += 2 * PI;
+    else if (an1 > PI) an1 -= 2 * PI;
+    /* set_control -> Nozzle.set_angles (src/robot.py:50-60, 173-185) */
+    SF(SALP_F_ANGLE1) = an1; SF(SALP_F_ANGLE2) = an2;
+    h.turn = fabs(an1 - pa1) / P.angle_speed + fabs(an2 - pa2) / P.angle_speed;
+    nozzle_direction(an1, an2, &h.d0);
+    /* set_control (src/robot.py:577-592, geometry.py:14-26) */
+    SF(SALP_F_CYCLE) = SF(SALP_F_CYCLE) + 1.0;
+    h.c = (double)r0;
+    h.coast = (double)r1;
+    h.ct = 0.0;
+    double sq = (double)sqf(r0);
+    h.refill = REFILL_C0 * sq + REFILL_C1 * h.c + REFILL_C2;
+    h.jet = PROPUL_C0 * sq + PROPUL_C1 * h.c + PROPUL_C2;
+    h.cr = h.refill > 0 ? h.c / h.refill : 0.0;
+    h.rr = h.jet > 0 ? h.c / h.jet : 0.0;
+    cycle_bounds(h);
+    /* step_through_cycle prologue (src/robot.py:742-748) */
+    const double total = h.b2;
+    double pq0 = SF(SALP_F_PPOS0), pq1 = SF(SALP_F_PPOS1), pq2 = SF(SALP_F_PPOS2);
+    double pg0 = SF(SALP_F_PANG0), pg1 = SF(SALP_F_PANG1), pg2 = SF(SALP_F_PANG2);
+    SF(SALP_F_AVGV0) = (h.q0 - pq0) / total; SF(SALP_F_AVGV1) = (h.q1 - pq1) / total;
+    SF(SALP_F_AVGV2) = (h.q2 - pq2) / total;
+    SF(SALP_F_AVGW0) = (h.g0 - pg0) / total; SF(SALP_F_AVGW1) = (h.g1 - pg1) / total;
+    SF(SALP_F_AVGW2) = (h.g2 - pg2) / total;
+    SF(SALP_F_PPOS0) = h.q0; SF(SALP_F_PPOS1) = h.q1; SF(SALP_F_PPOS2) = h.q2;
+    SF(SALP_F_PANG0) = h.g0; SF(SALP_F_PANG1) = h.g1; SF(SALP_F_PANG2) = h.g2;
+    SF(SALP_F_PENDING) = 1.0;
+}
+
+/* Resume an in-flight cycle: derived per-cycle values from stored ones. */
+SD void resume_cycle(Hot& h, const double* S, const Params& P, int64_t i) {
+    cycle_bounds(h);
+    nozzle_direction(SF(SALP_F_ANGLE1), SF(SALP_F_ANGLE2), &h.d0);
+}
+
+/* ------------------------------------------------------ observation */
+/* _get_observation (src/salp_robot_env.py:651-670) */
+SD void observation(const Hot& h, const Rot& R, const double* S, const Params& P, int64_t i,
+                    float* obs) {
+    double tx = SF(SALP_F_TARGET0), ty = SF(SALP_F_TARGET1);
+    double b0, b1;
+    rot_body_xy(R, tx - h.p0, ty - h.p1, &b0, &b1);
+    double heading = sm_atan2(b1, b0);
+    obs[0] = (float)b0; obs[1] = (float)b1;
+    obs[2] = (float)h.v0; obs[3] = (float)h.v1;
+    obs[4] = (float)h.w2; obs[5] = (float)heading;
+    const int nob = (int)SF(SALP_F_N_OBST);
+    for (int k = 0; k < P.num_obstacles; ++k) {
+        if (k < nob) {
+            obs[6 + 2 * k] = (float)(SF(SALP_F_OBST0 + 2 * k) - h.p0);
+            obs[7 + 2 * k] = (float)(SF(SALP_F_OBST0 + 2 * k + 1) - h.p1);
+        } else {
+            obs[6 + 2 * k] = 0.0f;
+            obs[7 + 2 * k] = 0.0f;
+        }
+    }
+}
+
+struct StepOut {
+    double reward;
+    bool terminated, truncated, hit;
+};
+
+/* ------------------------------------------------ env-step epilogue */
+/* SalpRobotEnv.step after the cycle (src/salp_robot_env.py:237-299), reward
+ * (:349-397), collision (:561-568), episode metrics (:399-447). */
+SD StepOut finish_step(const Hot& h, double* S, const Params& P, int64_t i, float* obs,
+                       double* info) {
+    StepOut out;
+    const Rot R = rot_zyx(h.e0, h.e1, h.e2);
+    double vw[3];
+    rot_apply(R, h.v0, h.v1, h.v2, vw);
+    const double px = h.p0, py = h.p1;
+    /* episode_positions / episode_velocities */
+    double path = SF(SALP_F_PATH_LEN) + np_norm2(px - SF(SALP_F_LAST_PX), py - SF(SALP_F_LAST_PY));
+    SF(SALP_F_PATH_LEN) = path;
+    SF(SALP_F_LAST_PX) = px; SF(SALP_F_LAST_PY) = py;
+    double svel = SF(SALP_F_SUM_VEL) + np_norm2(vw[0], vw[1]);
+    SF(SALP_F_SUM_VEL) = svel;
+    const double tx = SF(SALP_F_TARGET0), ty = SF(SALP_F_TARGET1);
+    const double dx = px - tx, dy = py - ty;
+    const double dist = np_norm2(dx, dy);
+    /* reward components */
+    double comp[7];
+    comp[0] = (-dist + SF(SALP_F_PREV_DIST)) * 100;
+    SF(SALP_F_PREV_DIST) = dist;
+    double b0, b1;
+    rot_body_xy(R, dx, dy, &b0, &b1);
+    comp[1] = -0.5 * fabs(sm_atan2(-b1, -b0));
+    const float a2 = (float)SF(SALP_F_ACT2);
+    const double ep_len = SF(SALP_F_EP_LEN);
+    if (ep_len == 0.0) {
+        double ch = (double)a2 - SF(SALP_F_PREV_A2);
+        comp[2] = -1.0 * (ch * ch);
+    } else {
+        float ch = a2 - (float)SF(SALP_F_PREV_A2);
+        comp[2] = (double)(-(ch * ch));
+    }
+    comp[3] = -10.0 * fabs(SF(SALP_F_AVGW2));
+    comp[4] = -0.1;
+    comp[5] = -100.0 * fabs(SF(SALP_F_AVGV1));
+    comp[6] = 0.0;
+    const int nob = (int)SF(SALP_F_N_OBST);
+    double md = 0.0;
+    for (int k = 0; k < nob; ++k) {
+        double d = np_norm2(px - SF(SALP_F_OBST0 + 2 * k), py - SF(SALP_F_OBST0 + 2 * k + 1));
+        if (k == 0 || d < md) md = d;
+    }
+    if (nob > 0) {
+        double danger = 2.0 * P.obstacle_radius;
+        if (md < danger) comp[6] = -1.0 * (1.0 - md / danger);
+    }
+    double reward = comp[0] + comp[1] + comp[2] + comp[3] + comp[4] + comp[5] + comp[6];
+    observation(h, R, S, P, i, obs);
+    /* _check_obstacle_collision with get_current_length() */
+    bool l32;
+    double Lc = body_length(P, h.phase, h.ct, h.refill, h.mx, h.c, h.cr, h.rr, &l32);
+    double thr = l32 ? (double)((float)P.obstacle_radius + (float)Lc / 2.0f)
+                     : P.obstacle_radius + Lc / 2;
+    bool hit = false;
+    for (int k = 0; k < nob; ++k) {
+        double d = np_norm2(px - SF(SALP_F_OBST0 + 2 * k), py - SF(SALP_F_OBST0 + 2 * k + 1));
+        if (d < thr) hit = true;
+    }
+    bool done = false, trunc = false;
+    if (dist < 0.2) { done = true; reward += 500.0; }
+    else if (dist > 5.0) { trunc = true; reward -= 200.0; }
+    if (hit) { trunc = true; reward -= 200.0; }
+    if (SF(SALP_F_CYCLE) >= (double)P.max_cycles) { trunc = true; reward -= 50.0; }
+    /* episode accumulators */
+    const double nlen = ep_len + 1.0;
+    SF(SALP_F_EP_LEN) = nlen;
+    const double ret = SF(SALP_F_EP_RETURN) + reward;
+    SF(SALP_F_EP_RETURN) = ret;
+    const double sa0 = SF(SALP_F_SUM_A0) + (double)(float)SF(SALP_F_ACT0);
+    const double sa1 = SF(SALP_F_SUM_A1) + (double)(float)SF(SALP_F_ACT1);
+    const double sa2 = SF(SALP_F_SUM_ABS_A2) + (double)fabsf(a2);
+    SF(SALP_F_SUM_A0) = sa0; SF(SALP_F_SUM_A1) = sa1; SF(SALP_F_SUM_ABS_A2) = sa2;
+    double sr[7];
+    for (int k = 0; k < 7; ++k) {
+        sr[k] = SF(SALP_F_SUM_R0 + k) + comp[k];
+        SF(SALP_F_SUM_R0 + k) = sr[k];
+    }
+    if (info) {
+        for (int k = 0; k < SALP_INFO_DIM; ++k) info[k] = 0.0;
+        for (int k = 0; k < 7; ++k) info[SALP_INFO_R_TRACK + k] = comp[k];
+        info[SALP_INFO_EP_RETURN] = ret;
+        info[SALP_INFO_EP_LEN] = nlen;
+        info[SALP_INFO_HIT_OBSTACLE] = hit ? 1.0 : 0.0;
+        if (done || trunc) {
+            double dd = np_norm2(px - 0.0, py - 0.0);
+            info[SALP_INFO_HAS_METRICS] = 1.0;
+            info[SALP_INFO_PATH_LENGTH] = path;
+            info[SALP_INFO_DIRECT_DISTANCE] = dd;
+            info[SALP_INFO_PATH_EFFICIENCY] = path > 0 ? dd / path : 0.0;
+            info[SALP_INFO_FINAL_DISTANCE] = dist;
+            info[SALP_INFO_INITIAL_DISTANCE] = SF(SALP_F_INIT_DIST);
+            info[SALP_INFO_AVG_COMPRESSION] = sa0 / nlen;
+            info[SALP_INFO_AVG_COAST_TIME] = sa1 / nlen;
+            info[SALP_INFO_AVG_NOZZLE_ANGLE] = sa2 / nlen;
+            info[SALP_INFO_AVG_VELOCITY] = svel / (nlen + 1.0);
+            for (int k = 0; k < 7; ++k) info[SALP_INFO_AVG_R_TRACK + k] = sr[k] / nlen;
+        }
+    }
+    SF(SALP_F_PREV_A2) = (double)a2;
+    SF(SALP_F_PENDING) = 0.0;
+    out.reward = reward;
+    out.terminated = done;
+    out.truncated = trunc;
+    out.hit = hit;
+    return out;
+}
+
+/* ---------------------------------------------------------- reset */
+/* Philox draws replacing np.random in generate_target_point("random") and
+ * _generate_obstacles (src/salp_robot_env.py:449-559). */
+SD int draw_reset(const Params& P, uint64_t env_id, uint64_t episode, float* tgt, float* obst) {
+    double u0, u1;
+    sp_reset_pair(P.seed, env_id, episode, 0u, &u0, &u1);
+    double tx = P.x_min + (P.x_max - P.x_min) * u0, ty = P.y_min + (P.y_max - P.y_min) * u1;
+    if (tx < P.x_min) tx = P.x_min;
+    if (tx > P.x_max) tx = P.x_max;
+    if (ty < P.y_min) ty = P.y_min;
+    if (ty > P.y_max) ty = P.y_max;
+    tgt[0] = (float)tx; tgt[1] = (float)ty;
+    int n = 0;
+    for (int k = 0; k < P.num_obstacles; ++k) {
+        for (int att = 0; att < 200; ++att) {
+            sp_reset_pair(P.seed, env_id, episode, (uint32_t)(1 + k * 200 + att), &u0, &u1);
+            float px = (float)(P.x_min + (P.x_max - P.x_min) * u0);
+            float py = (float)(P.y_min + (P.y_max - P.y_min) * u1);
+            float ds = sqrtf(sm_fmaf(py, py, px * px));
+            float ex = px - tgt[0], ey = py - tgt[1];
+            float dtg = sqrtf(sm_fmaf(ey, ey, ex * ex));
+            bool close = false;
+            for (int j = 0; j < n; ++j) {
+                float fx = px - obst[2 * j], fy = py - obst[2 * j + 1];
+                if ((double)sqrtf(sm_fmaf(fy, fy, fx * fx)) < P.sep) close = true;
+            }
+            if ((double)ds > 0.5 && (double)dtg > 0.5 && !close) {
+                obst[2 * n] = px; obst[2 * n + 1] = py; ++n;
+                break;
+            }
+        }
+    }
+    return n;
+}
+
+/* SalpRobotEnv.reset with the target / obstacles given (src/salp_robot_env.py:
+ * 114-155) -> Robot.reset (src/robot.py:452-501). */
+SD void reset_env(Hot& h, double* S, const Params& P, int64_t i, const float* tgt,
+                  const float* obst, int nob, float* obs) {
+    SF(SALP_F_TARGET0) = tgt[0]; SF(SALP_F_TARGET1) = tgt[1];
+    for (int k = 0; k < SALP_MAX_OBSTACLES; ++k) {
+        SF(SALP_F_OBST0 + 2 * k) = k < nob ? (double)obst[2 * k] : 0.0;
+        SF(SALP_F_OBST0 + 2 * k + 1) = k < nob ? (double)obst[2 * k + 1] : 0.0;
+    }
+    SF(SALP_F_N_OBST) = nob;
+    /* Robot.reset: kinematics zeroed; COM from the PREVIOUS geometry */
+    h.time = 0.0; h.ct = 0.0; h.phase = REST;
+    SF(SALP_F_CYCLE) = 0.0;
+    h.v0 = h.v1 = h.v2 = 0.0; h.w0 = h.w1 = h.w2 = 0.0;
+    h.a0 = h.a1 = h.a2 = 0.0; h.al0 = h.al1 = h.al2 = 0.0;
+    h.e0 = h.e1 = h.e2 = 0.0; h.p0 = h.p1 = h.p2 = 0.0;
+    h.q0 = h.q1 = h.q2 = 0.0; h.g0 = h.g1 = h.g2 = 0.0;
+    SF(SALP_F_PPOS0) = 0.0; SF(SALP_F_PPOS1) = 0.0; SF(SALP_F_PPOS2) = 0.0;
+    SF(SALP_F_PANG0) = 0.0; SF(SALP_F_PANG1) = 0.0; SF(SALP_F_PANG2) = 0.0;
+    h.com = center_of_mass(P, h.L, h.W, water_mass(P, h.V, h.g32), h.g32);
+    h.comr = (h.com - h.com) / DT;
+    h.coma = (h.comr - h.comr) / DT;
+    h.L = P.L0; h.W = P.W0; h.g32 = false;
+    h.V = water_volume(P, h.L, h.W, false);
+    h.pV = h.V; h.pv32 = false;
+    Geo g = geometry(P, h.L, h.W, h.V, h.pV, false, false);
+    h.pI0 = g.I0; h.pI1 = g.I1; h.pI2 = g.I1;
+    /* env trackers */
+    const double d0 = h.p0 - (double)tgt[0], d1 = h.p1 - (double)tgt[1];
+    const double dist = np_norm2(d0, d1);
+    SF(SALP_F_PREV_DIST) = dist;
+    SF(SALP_F_PREV_A2) = 0.0;
+    SF(SALP_F_ACT0) = 0.0; SF(SALP_F_ACT1) = 0.0; SF(SALP_F_ACT2) = 0.0;
+    SF(SALP_F_EP_LEN) = 0.0; SF(SALP_F_EP_RETURN) = 0.0; SF(SALP_F_PATH_LEN) = 0.0;
+    SF(SALP_F_LAST_PX) = h.p0; SF(SALP_F_LAST_PY) = h.p1;
+    SF(SALP_F_SUM_A0) = 0.0; SF(SALP_F_SUM_A1) = 0.0; SF(SALP_F_SUM_ABS_A2) = 0.0;
+    SF(SALP_F_SUM_VEL) = np_norm2(0.0, 0.0);
+    SF(SALP_F_INIT_DIST) = dist;
+    for (int k = 0; k < 7; ++k) SF(SALP_F_SUM_R0 + k) = 0.0;
+    SF(SALP_F_EPISODE) = SF(SALP_F_EPISODE) + 1.0;
+    SF(SALP_F_PENDING) = 0.0;
+    if (obs) {
+        Rot R = rot_zyx(h.e0, h.e1, h.e2);
+        observation(h, R, S, P, i, obs);
+    }
+}
+
+SD void reset_env_philox(Hot& h, double* S, const Params& P, int64_t i, float* obs) {
+    float tgt[2], obst[2 * SALP_MAX_OBSTACLES];
+    int nob = draw_reset(P, (uint64_t)(P.env_offset + i), (uint64_t)SF(SALP_F_EPISODE), tgt, obst);
+    reset_env(h, S, P, i, tgt, obst, nob, obs);
+}
+
+/* Robot / Nozzle / SalpRobotEnv constructors (src/robot.py:20-47, 261-412) */
+SD void construct_env(double* S, const Params& P, int64_t i) {
+    for (int f = 0; f < SALP_NUM_FIELDS; ++f) SF(f) = 0.0;
+    Hot h;
+    h.L = P.L0; h.W = P.W0; h.g32 = false; h.pv32 = false;
+    h.V = water_volume(P, h.L, h.W, false);
+    h.pV = h.V;
+    Geo g = geometry(P, h.L, h.W, h.V, h.pV, false, false);
+    SF(SALP_F_LENGTH) = h.L; SF(SALP_F_WIDTH) = h.W;
+    SF(SALP_F_VOLUME) = h.V; SF(SALP_F_PREV_VOLUME) = h.pV;
+    SF(SALP_F_PREV_I0) = g.I0; SF(SALP_F_PREV_I1) = g.I1; SF(SALP_F_PREV_I2) = g.I1;
+    /* Robot.__init__ runs before set_environment: density 1000 */
+    SF(SALP_F_COM) = center_of_mass(P, h.L, h.W, 1000.0 * h.V, false);
+    SF(SALP_F_PHASE) = REST;
+    /* make_env: nozzle.set_angles(init angles) */
+    SF(SALP_F_ANGLE1) = P.init_angle1; SF(SALP_F_ANGLE2) = P.init_angle2;
+    SF(SALP_F_TURN_TIME) = fabs(P.init_angle1 - 0.0) / P.angle_speed +
+                           fabs(P.init_angle2 - 0.0) / P.angle_speed;
+}
+
+#undef SF
+}  // namespace salp
+
+#endif /* SALP_DEVICE_H */

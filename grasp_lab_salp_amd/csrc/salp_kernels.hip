@@ -1,0 +1,408 @@
+// salp_kernels.hip — HIP kernels for gfx950 + the C ABI of include/salp.h.
+//
+// One env per lane, struct-of-arrays fp64 state in HBM.  Every kernel loads a
+// lane's hot state once, runs whole breathing cycles (hundreds of physics
+// ticks) in registers, and stores once; the only HBM traffic inside a cycle
+// is nothing at all.  See DESIGN.md for the data layout and roofline.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "salp_device.h"
+
+using salp::Hot;
+using salp::Params;
+
+#define SF(f) S[(size_t)(f) * (size_t)P.n + (size_t)i]
+
+namespace {
+
+constexpr int kBlock = 256;
+// Longest legitimate cycle: max(refill 3.3 s, turn 3.9 s) + jet 0.5 s + coast
+// 10 s < 1500 ticks.  The guard only bounds a lane fed a corrupted state.
+constexpr int kMaxTicksPerCycle = 1 << 16;
+
+__device__ __forceinline__ void run_cycle(Hot& h, const Params& P) {
+    for (int g = 0; h.ct < h.b2 && g < kMaxTicksPerCycle; ++g) salp::tick(h, P);
+}
+
+__global__ __launch_bounds__(kBlock) void k_construct(double* S, Params P) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    salp::construct_env(S, P, i);
+}
+
+__global__ __launch_bounds__(kBlock) void k_reset(double* S, Params P, const uint8_t* mask,
+                                                  float* obs) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n || (mask && !mask[i])) return;
+    Hot h;
+    salp::load_hot(h, S, P, i);
+    float o[SALP_OBS_DIM_MAX];
+    salp::reset_env_philox(h, S, P, i, o);
+    salp::store_hot(h, S, P, i);
+    if (obs)
+        for (int k = 0; k < P.obs_dim; ++k) obs[(size_t)i * P.obs_dim + k] = o[k];
+}
+
+__global__ __launch_bounds__(kBlock) void k_reset_to(double* S, Params P, const uint8_t* mask,
+                                                     const float* tgt, const float* obst,
+                                                     const int32_t* nob, float* obs) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n || (mask && !mask[i])) return;
+    Hot h;
+    salp::load_hot(h, S, P, i);
+    float o[SALP_OBS_DIM_MAX];
+    int n = nob[i];
+    n = n < 0 ? 0 : (n > P.num_obstacles ? P.num_obstacles : n);
+    salp::reset_env(h, S, P, i, tgt + 2 * i, obst + 2 * SALP_MAX_OBSTACLES * i, n, o);
+    salp::store_hot(h, S, P, i);
+    if (obs)
+        for (int k = 0; k < P.obs_dim; ++k) obs[(size_t)i * P.obs_dim + k] = o[k];
+}
+
+// SalpRobotEnv.step for every env (one breathing cycle each).
+__global__ __launch_bounds__(kBlock) void k_step(double* S, Params P, const float* actions,
+                                                 float* obs_out, double* reward_out,
+                                                 uint8_t* term_out, uint8_t* trunc_out,
+                                                 int auto_reset, float* term_obs_out,
+                                                 double* info_out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    Hot h;
+    salp::load_hot(h, S, P, i);
+    salp::begin_step(h, S, P, i, actions[3 * i], actions[3 * i + 1], actions[3 * i + 2]);
+    run_cycle(h, P);
+    SF(SALP_F_STEP_COUNT) = SF(SALP_F_STEP_COUNT) + 1.0;
+    float o[SALP_OBS_DIM_MAX];
+    salp::StepOut r = salp::finish_step(h, S, P, i, o, info_out ? info_out + (size_t)SALP_INFO_DIM * i : nullptr);
+    if (reward_out) reward_out[i] = r.reward;
+    if (term_out) term_out[i] = r.terminated;
+    if (trunc_out) trunc_out[i] = r.truncated;
+    if (term_obs_out)
+        for (int k = 0; k < P.obs_dim; ++k) term_obs_out[(size_t)i * P.obs_dim + k] = o[k];
+    if (auto_reset && (r.terminated || r.truncated)) salp::reset_env_philox(h, S, P, i, o);
+    if (obs_out)
+        for (int k = 0; k < P.obs_dim; ++k) obs_out[(size_t)i * P.obs_dim + k] = o[k];
+    salp::store_hot(h, S, P, i);
+}
+
+// Lock-step random-action env steps (every env does exactly n_steps).
+__global__ __launch_bounds__(kBlock) void k_step_random(double* S, Params P, int32_t n_steps,
+                                                        double* reward_sum) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    Hot h;
+    salp::load_hot(h, S, P, i);
+    const uint64_t env_id = (uint64_t)(P.env_offset + i);
+    double rs = 0.0;
+    for (int32_t k = 0; k < n_steps; ++k) {
+        float a[3];
+        sp_action(P.seed, env_id, (uint64_t)SF(SALP_F_STEP_COUNT), a);
+        salp::begin_step(h, S, P, i, a[0], a[1], a[2]);
+        run_cycle(h, P);
+        SF(SALP_F_STEP_COUNT) = SF(SALP_F_STEP_COUNT) + 1.0;
+        float o[SALP_OBS_DIM_MAX];
+        salp::StepOut r = salp::finish_step(h, S, P, i, o, nullptr);
+        rs += r.reward;
+        if (r.terminated || r.truncated) salp::reset_env_philox(h, S, P, i, o);
+    }
+    if (reward_sum) reward_sum[i] = rs;
+    salp::store_hot(h, S, P, i);
+}
+
+// Chained random-action rollout under a per-lane tick budget, filling the
+// rollout buffer.  A lane finishes the env-step whose cycle ends, immediately
+// starts the next one, and never idles while other lanes of its wave are still
+// inside a long cycle.
+__global__ __launch_bounds__(kBlock) void k_rollout(double* S, Params P, int64_t tick_budget,
+                                                    int64_t max_steps, SalpRolloutBuffers B) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    Hot h;
+    salp::load_hot(h, S, P, i);
+    const uint64_t env_id = (uint64_t)(P.env_offset + i);
+    bool pending = SF(SALP_F_PENDING) != 0.0;
+    if (pending) salp::resume_cycle(h, S, P, i);
+    int64_t steps = B.steps_done ? B.steps_done[i] : 0;
+    int64_t ticks = 0, events = 0;
+    for (;;) {
+        if (pending && !(h.ct < h.b2)) {
+            SF(SALP_F_STEP_COUNT) = SF(SALP_F_STEP_COUNT) + 1.0;
+            float o[SALP_OBS_DIM_MAX];
+            salp::StepOut r = salp::finish_step(h, S, P, i, o, nullptr);
+            if (B.capacity > 0) {
+                const size_t slot = (size_t)(steps % B.capacity);
+                const size_t row = slot * (size_t)P.n + (size_t)i;
+                if (B.obs)
+                    for (int k = 0; k < P.obs_dim; ++k) B.obs[row * P.obs_dim + k] = o[k];
+                if (B.actions) {
+                    B.actions[row * 3 + 0] = (float)SF(SALP_F_ACT0);
+                    B.actions[row * 3 + 1] = (float)SF(SALP_F_ACT1);
+                    B.actions[row * 3 + 2] = (float)SF(SALP_F_ACT2);
+                }
+                if (B.rewards) B.rewards[row] = (float)r.reward;
+                if (B.dones) B.dones[row] = (uint8_t)((r.terminated ? 1 : 0) | (r.truncated ? 2 : 0));
+            }
+            ++steps;
+            ++events;
+            pending = false;
+            if (r.terminated || r.truncated) salp::reset_env_philox(h, S, P, i, nullptr);
+        }
+        if (!pending) {
+            if ((max_steps > 0 && steps >= max_steps) || events > tick_budget) break;
+            float a[3];
+            sp_action(P.seed, env_id, (uint64_t)SF(SALP_F_STEP_COUNT), a);
+            salp::begin_step(h, S, P, i, a[0], a[1], a[2]);
+            pending = true;
+            continue;
+        }
+        if (ticks >= tick_budget) break;
+        salp::tick(h, P);
+        ++ticks;
+    }
+    if (B.steps_done) B.steps_done[i] = steps;
+    salp::store_hot(h, S, P, i);
+}
+
+__global__ void k_math_selftest(const double* x, const double* y, int64_t n, double* out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[0 * n + i] = sm_sin(x[i]);
+    out[1 * n + i] = sm_cos(x[i]);
+    out[2 * n + i] = sm_tan(x[i]);
+    out[3 * n + i] = sm_atan2(x[i], y[i]);
+    out[4 * n + i] = sm_asin(x[i]);
+    out[5 * n + i] = sm_acos(x[i]);
+    out[6 * n + i] = sm_cube(x[i]);
+    float s, c;
+    sm_np_sincosf((float)x[i], &s, &c);
+    out[7 * n + i] = c;
+    out[8 * n + i] = s;
+}
+
+const char* const kFieldNames[SALP_NUM_FIELDS] = {
+    "v0", "v1", "v2", "w0", "w1", "w2", "acc0", "acc1", "acc2", "alpha0", "alpha1", "alpha2",
+    "eta0", "eta1", "eta2", "pw0", "pw1", "pw2", "pos0", "pos1", "pos2", "ang0", "ang1", "ang2",
+    "ppos0", "ppos1", "ppos2", "pang0", "pang1", "pang2", "avgv0", "avgv1", "avgv2",
+    "avgw0", "avgw1", "avgw2",
+    "length", "width", "volume", "prev_volume", "com", "com_rate", "com_acc",
+    "prev_I0", "prev_I1", "prev_I2", "geom32", "pvol32",
+    "cycle_time", "time", "refill_time", "jet_time", "coast_time", "contraction",
+    "contract_rate", "release_rate", "phase", "cycle",
+    "angle1", "angle2", "yaw", "prev_yaw", "turn_time",
+    "target0", "target1", "obst0", "obst1", "obst2", "obst3", "obst4", "obst5", "obst6", "obst7",
+    "n_obst", "prev_dist", "prev_a2",
+    "ep_len", "ep_return", "path_len", "last_px", "last_py", "sum_a0", "sum_a1", "sum_abs_a2",
+    "sum_vel", "init_dist", "sum_r0", "sum_r1", "sum_r2", "sum_r3", "sum_r4", "sum_r5", "sum_r6",
+    "act0", "act1", "act2", "pending", "step_count", "episode"};
+
+thread_local std::string g_last_error;
+
+}  // namespace
+
+struct SalpEnv {
+    int device = 0;
+    int64_t n = 0;
+    SalpParams params{};
+    Params dp{};
+    double* state = nullptr;
+    std::string err;
+};
+
+namespace {
+
+int fail(SalpEnv* h, int code, const std::string& msg) {
+    if (h) h->err = msg;
+    g_last_error = msg;
+    return code;
+}
+
+int check_hip(SalpEnv* h, hipError_t e, const char* what) {
+    if (e == hipSuccess) return SALP_OK;
+    return fail(h, SALP_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int launched(SalpEnv* h, const char* what) { return check_hip(h, hipGetLastError(), what); }
+
+unsigned blocks_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+// Launch-invariant constants; the same IEEE expressions as the oracle.
+Params derive(const SalpParams& p, int64_t n, uint64_t seed, int64_t offset) {
+    Params d{};
+    const double PI = salp::PI;
+    d.L0 = p.init_length; d.W0 = p.init_width; d.maxc = p.max_contraction;
+    d.dry_mass = p.dry_mass; d.nozzle_mass = p.nozzle_mass; d.density = p.density;
+    d.nozzle_area = p.nozzle_area;
+    d.mid_x = -(p.nozzle_length1 + p.nozzle_length2);
+    d.tube_volume = PI * (0.029 * 0.029) * 0.15;
+    d.tube_volume_I = 3.14159265358979 * (0.029 * 0.029) * 0.15;
+    d.net_tube_mass = salp::TUBE_MASS - d.tube_volume_I * 1000.0;
+    d.com_mass_sum = salp::TUBE_MASS + p.nozzle_mass + salp::BUOY_MASS + salp::SKIN_MASS;
+    d.P1000tv = 1000.0 * d.tube_volume;
+    d.init_aspect = p.init_length / p.init_width;
+    double cl = p.init_length - p.max_contraction;
+    double cw = p.init_length - cl + p.init_width;
+    d.end_aspect = cl / cw;
+    d.aspect_den = d.init_aspect - d.end_aspect;
+    d.angle_speed = 31 * PI / 30;
+    d.obstacle_radius = p.obstacle_radius;
+    const double scale = 200.0, margin = 50;
+    d.x_min = (-p.width / 2.0 + margin) / scale;
+    d.x_max = (p.width / 2.0 - margin) / scale;
+    d.y_min = (-p.height / 2.0 + margin) / scale;
+    d.y_max = (p.height / 2.0 - margin) / scale;
+    d.sep = 2 * p.obstacle_radius + 0.1;
+    d.init_angle1 = p.init_angle1; d.init_angle2 = p.init_angle2;
+    d.num_obstacles = p.num_obstacles;
+    d.max_cycles = p.max_cycles;
+    d.obs_dim = 6 + 2 * p.num_obstacles;
+    d.n = n;
+    d.env_offset = offset;
+    d.seed = seed;
+    return d;
+}
+
+}  // namespace
+
+extern "C" {
+
+int salp_abi_version(void) { return SALP_ABI_VERSION; }
+
+void salp_default_params(SalpParams* p) {
+    std::memset(p, 0, sizeof *p);
+    p->nozzle_length1 = 0.05; p->nozzle_length2 = 0.05; p->nozzle_length3 = 0.05;
+    p->nozzle_area = 0.00016; p->nozzle_mass = 1.0;
+    p->dry_mass = 1.0; p->init_length = 0.3; p->init_width = 0.15; p->max_contraction = 0.06;
+    p->density = 1000.0; p->init_angle1 = 0.0; p->init_angle2 = 0.0;
+    p->obstacle_radius = 0.2; p->width = 900; p->height = 700; p->num_obstacles = 2;
+    p->max_cycles = 500;
+}
+
+int salp_create(const SalpParams* p, int64_t n_envs, uint64_t seed, int64_t env_id_offset,
+                int device, SalpEnv** out) {
+    if (!p || !out) return fail(nullptr, SALP_EINVAL, "salp_create: null argument");
+    *out = nullptr;
+    if (n_envs <= 0) return fail(nullptr, SALP_EINVAL, "salp_create: n_envs must be positive");
+    if (p->num_obstacles < 0 || p->num_obstacles > SALP_MAX_OBSTACLES)
+        return fail(nullptr, SALP_EINVAL, "salp_create: num_obstacles must be in [0, 4]");
+    if (!(p->init_length > 0) || !(p->init_width > 0) || !(p->nozzle_area > 0))
+        return fail(nullptr, SALP_EINVAL, "salp_create: non-positive body dimensions");
+    auto* h = new SalpEnv();
+    h->device = device;
+    h->n = n_envs;
+    h->params = *p;
+    h->dp = derive(*p, n_envs, seed, env_id_offset);
+    int rc = check_hip(nullptr, hipSetDevice(device), "hipSetDevice");
+    if (rc) { delete h; return rc; }
+    rc = check_hip(nullptr, hipMalloc(&h->state, sizeof(double) * SALP_NUM_FIELDS * (size_t)n_envs),
+                   "hipMalloc(state)");
+    if (rc) { delete h; return SALP_ENOMEM; }
+    hipLaunchKernelGGL(k_construct, dim3(blocks_for(n_envs)), dim3(kBlock), 0, nullptr, h->state, h->dp);
+    if ((rc = launched(h, "k_construct"))) { g_last_error = h->err; salp_destroy(h); return rc; }
+    // SalpRobotEnv.__init__ ends with self.reset() (src/salp_robot_env.py:112)
+    hipLaunchKernelGGL(k_reset, dim3(blocks_for(n_envs)), dim3(kBlock), 0, nullptr, h->state, h->dp,
+                       (const uint8_t*)nullptr, (float*)nullptr);
+    if ((rc = launched(h, "k_reset"))) { g_last_error = h->err; salp_destroy(h); return rc; }
+    if ((rc = check_hip(h, hipDeviceSynchronize(), "salp_create sync"))) {
+        g_last_error = h->err; salp_destroy(h); return rc;
+    }
+    *out = h;
+    return SALP_OK;
+}
+
+int salp_destroy(SalpEnv* h) {
+    if (!h) return SALP_OK;
+    if (h->state) {
+        (void)hipSetDevice(h->device);
+        (void)hipFree(h->state);
+    }
+    delete h;
+    return SALP_OK;
+}
+
+const char* salp_last_error(const SalpEnv* h) {
+    return h ? h->err.c_str() : g_last_error.c_str();
+}
+
+int64_t salp_num_envs(const SalpEnv* h) { return h ? h->n : -1; }
+int salp_obs_dim(const SalpEnv* h) { return h ? h->dp.obs_dim : -1; }
+int salp_num_fields(void) { return SALP_NUM_FIELDS; }
+const char* salp_field_name(int f) {
+    return (f >= 0 && f < SALP_NUM_FIELDS) ? kFieldNames[f] : nullptr;
+}
+
+int salp_reset(SalpEnv* h, const uint8_t* mask, float* obs_out, void* stream) {
+    if (!h) return fail(nullptr, SALP_EINVAL, "salp_reset: null handle");
+    hipLaunchKernelGGL(k_reset, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream,
+                       h->state, h->dp, mask, obs_out);
+    return launched(h, "k_reset");
+}
+
+int salp_reset_to(SalpEnv* h, const uint8_t* mask, const float* targets, const float* obstacles,
+                  const int32_t* n_obstacles, float* obs_out, void* stream) {
+    if (!h) return fail(nullptr, SALP_EINVAL, "salp_reset_to: null handle");
+    if (!targets || !obstacles || !n_obstacles)
+        return fail(h, SALP_EINVAL, "salp_reset_to: targets, obstacles and n_obstacles are required");
+    hipLaunchKernelGGL(k_reset_to, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream,
+                       h->state, h->dp, mask, targets, obstacles, n_obstacles, obs_out);
+    return launched(h, "k_reset_to");
+}
+
+int salp_step(SalpEnv* h, const float* actions, float* obs_out, double* reward_out,
+              uint8_t* terminated_out, uint8_t* truncated_out, int auto_reset,
+              float* terminal_obs_out, double* info_out, void* stream) {
+    if (!h) return fail(nullptr, SALP_EINVAL, "salp_step: null handle");
+    if (!actions) return fail(h, SALP_EINVAL, "salp_step: actions is required");
+    hipLaunchKernelGGL(k_step, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream,
+                       h->state, h->dp, actions, obs_out, reward_out, terminated_out, truncated_out,
+                       auto_reset, terminal_obs_out, info_out);
+    return launched(h, "k_step");
+}
+
+int salp_step_random(SalpEnv* h, int32_t n_steps, double* reward_sum_out, void* stream) {
+    if (!h) return fail(nullptr, SALP_EINVAL, "salp_step_random: null handle");
+    if (n_steps < 0) return fail(h, SALP_EINVAL, "salp_step_random: n_steps < 0");
+    hipLaunchKernelGGL(k_step_random, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream,
+                       h->state, h->dp, n_steps, reward_sum_out);
+    return launched(h, "k_step_random");
+}
+
+int salp_rollout(SalpEnv* h, int64_t tick_budget, const SalpRolloutBuffers* buf, void* stream) {
+    if (!h) return fail(nullptr, SALP_EINVAL, "salp_rollout: null handle");
+    if (tick_budget < 0) return fail(h, SALP_EINVAL, "salp_rollout: tick_budget < 0");
+    SalpRolloutBuffers b{};
+    if (buf) b = *buf;
+    if (b.capacity < 0) return fail(h, SALP_EINVAL, "salp_rollout: capacity < 0");
+    hipLaunchKernelGGL(k_rollout, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream,
+                       h->state, h->dp, tick_budget, b.max_steps, b);
+    return launched(h, "k_rollout");
+}
+
+int salp_get_state(SalpEnv* h, double* state_out, void* stream) {
+    if (!h || !state_out) return fail(h, SALP_EINVAL, "salp_get_state: null argument");
+    return check_hip(h, hipMemcpyAsync(state_out, h->state, sizeof(double) * SALP_NUM_FIELDS * (size_t)h->n,
+                                       hipMemcpyDeviceToDevice, (hipStream_t)stream),
+                     "salp_get_state");
+}
+
+int salp_set_state(SalpEnv* h, const double* state_in, void* stream) {
+    if (!h || !state_in) return fail(h, SALP_EINVAL, "salp_set_state: null argument");
+    return check_hip(h, hipMemcpyAsync(h->state, state_in, sizeof(double) * SALP_NUM_FIELDS * (size_t)h->n,
+                                       hipMemcpyDeviceToDevice, (hipStream_t)stream),
+                     "salp_set_state");
+}
+
+int salp_math_selftest(const double* x, const double* y, int64_t n, double* out, void* stream) {
+    if (!x || !y || !out || n < 0) return fail(nullptr, SALP_EINVAL, "salp_math_selftest: bad argument");
+    hipLaunchKernelGGL(k_math_selftest, dim3(blocks_for(n)), dim3(kBlock), 0, (hipStream_t)stream, x, y,
+                       n, out);
+    return check_hip(nullptr, hipGetLastError(), "k_math_selftest");
+}
+
+int64_t salp_state_ptr(SalpEnv* h) { return h ? (int64_t)(intptr_t)h->state : 0; }
+
+}  // extern "C"

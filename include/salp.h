@@ -90,6 +90,8 @@ typedef struct SalpRolloutBuffers {
     float* rewards;        /* [capacity][n_envs]  (float32, SB3 buffer dtype)  */
     uint8_t* dones;        /* [capacity][n_envs]  bit0 terminated, bit1 truncated */
     int64_t* steps_done;   /* [n_envs] completed env-steps counter (in/out)    */
+    int64_t max_steps;     /* >0: a lane starts no env-step once steps_done
+                            * reaches it (fixed-length rollouts, n_steps)     */
 } SalpRolloutBuffers;
 
 /* ------------------------------------------------------------ lifecycle */
@@ -138,6 +140,8 @@ int salp_num_fields(void);
 const char* salp_field_name(int field);
 int salp_get_state(SalpEnv* h, double* state_out, void* stream);
 int salp_set_state(SalpEnv* h, const double* state_in, void* stream);
+/* Device address of the handle's state buffer (zero-copy views). */
+int64_t salp_state_ptr(SalpEnv* h);
 /* Device-side self-test of salp_math.h: out[i] = f(x[i]) for f in
  * {sin, cos, tan, atan2(x, y), asin, acos, cube, np_cosf, np_sinf}.
  * x, y [n]; out [9][n]. */

@@ -1,0 +1,221 @@
+"""Device (libsalp.so, gfx950) against the CPU oracle — bit for bit.
+
+The oracle is pinned to the reference by tests/test_oracle_golden.py; here the
+HIP path must reproduce the oracle EXACTLY (np.array_equal on fp64 state,
+float32 observations, fp64 rewards, flags).  Everything goes through the C ABI
+via grasp_lab_salp_amd.batched_env.
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import COMPARED, load_episodes, snapshot_to_state
+from grasp_lab_salp_amd._abi import FIELD, FIELDS, INFO, NUM_FIELDS, default_params
+from grasp_lab_salp_amd.batched_env import BatchedSalpEnv
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _cpu(t):
+    return t.detach().cpu().numpy()
+
+
+def assert_state_equal(gpu_state, cpu_state, what=""):
+    g = _cpu(gpu_state) if torch.is_tensor(gpu_state) else gpu_state
+    bad = [(FIELDS[f], int(np.sum(g[f] != cpu_state[f]))) for f in range(NUM_FIELDS)
+           if not np.array_equal(g[f], cpu_state[f])]
+    assert not bad, f"{what}: state fields differ from the oracle: {bad[:8]}"
+
+
+def make_pair(n, seed=3, **kw):
+    p = default_params(**kw)
+    env = BatchedSalpEnv(n, params=p, seed=seed)
+    o = orc.Oracle(p, n, seed=seed)
+    return env, o
+
+
+def random_actions(rng, n):
+    return np.stack([rng.uniform(0, 1, n), rng.uniform(0, 1, n), rng.uniform(-1, 1, n)],
+                    1).astype(np.float32)
+
+
+def test_device_math_equals_oracle_math():
+    rng = np.random.default_rng(0)
+    x = np.concatenate([rng.uniform(-4, 4, 20000), rng.uniform(-1, 1, 20000),
+                        rng.uniform(-1e-4, 1e-4, 2000), rng.uniform(-80, 80, 2000),
+                        [0.0, 1.0, -1.0, 0.5, np.pi / 4, np.pi / 2]])
+    y = rng.uniform(-3, 3, len(x))
+    from grasp_lab_salp_amd import _lib
+    import ctypes
+    L = _lib.load()
+    xd = torch.tensor(x, device="cuda")
+    yd = torch.tensor(y, device="cuda")
+    out = torch.empty((9, len(x)), dtype=torch.float64, device="cuda")
+    _lib.check(L.salp_math_selftest(ctypes.c_void_p(xd.data_ptr()), ctypes.c_void_p(yd.data_ptr()),
+                                    len(x), ctypes.c_void_p(out.data_ptr()), None))
+    torch.cuda.synchronize()
+    ref = orc.math_selftest(x, y)
+    g = _cpu(out)
+    for r in range(9):
+        assert np.array_equal(g[r], ref[r]), f"math row {r}: {np.sum(g[r] != ref[r])} mismatches"
+
+
+def test_fresh_envs_equal_oracle():
+    env, o = make_pair(1000)
+    o.reset()  # SalpRobotEnv.__init__ -> reset()
+    assert_state_equal(env.get_state(), o.state, "after create")
+    ob = env.reset()
+    ob_o = o.reset()
+    assert np.array_equal(_cpu(ob), ob_o)
+    assert_state_equal(env.get_state(), o.state, "after reset")
+
+
+@pytest.mark.parametrize("K", [0, 2, 4])
+def test_teacher_forced_golden_rows(K):
+    """Restart from every reference pre-step state of the golden fixture."""
+    d = load_episodes()
+    rows = np.where(d["num_obstacles_cfg"] == K)[0]
+    p = default_params(num_obstacles=K)
+    st = snapshot_to_state(d, "b_", rows)
+    env = BatchedSalpEnv(len(rows), params=p)
+    env.set_state(torch.tensor(st))
+    o = orc.Oracle(p, len(rows))
+    o.state[:] = st
+    r = env.step(torch.tensor(d["action"][rows]), auto_reset=False)
+    ro = o.step(d["action"][rows])
+    assert_state_equal(env.get_state(), o.state, f"golden K={K}")
+    assert np.array_equal(_cpu(r.obs), ro["obs"])
+    assert np.array_equal(_cpu(r.reward), ro["reward"])
+    assert np.array_equal(_cpu(r.terminated).astype(np.uint8), ro["terminated"])
+    assert np.array_equal(_cpu(r.truncated).astype(np.uint8), ro["truncated"])
+    assert np.array_equal(_cpu(r.info), ro["info"])
+    # and directly against the reference itself (same tolerances as the oracle tests)
+    after = snapshot_to_state(d, "a_", rows)
+    g = _cpu(env.get_state())
+    for name in ("pw0", "pw1", "v0", "v1", "eta2", "w2", "length", "cycle_time", "phase"):
+        i = FIELD[name]
+        floor = 1e-6 * np.max(np.abs(after[i])) + 1e-300
+        assert np.max(np.abs(g[i] - after[i]) / np.maximum(np.abs(after[i]), floor)) <= 2e-6, name
+    assert np.array_equal(_cpu(r.terminated), d["terminated"][rows].astype(bool))
+    assert np.array_equal(_cpu(r.truncated), d["truncated"][rows].astype(bool))
+
+
+def test_random_batch_free_running_with_auto_reset():
+    """4096 envs, injected targets/obstacles, 6 env-steps of random float32
+    actions, SB3-style auto-reset (Philox draws on both sides)."""
+    n = 4096
+    rng = np.random.default_rng(11)
+    env, o = make_pair(n, seed=5)
+    o.reset()
+    tg = np.stack([rng.uniform(-2, 2, n), rng.uniform(-1.5, 1.5, n)], 1).astype(np.float32)
+    ob = rng.uniform(-2, 2, (n, 2, 2)).astype(np.float32)
+    nob = rng.integers(0, 3, n).astype(np.int32)
+    obs_g = env.reset_to(torch.tensor(tg), torch.tensor(ob), torch.tensor(nob))
+    obs_o = o.reset_to(tg, ob, nob)
+    assert np.array_equal(_cpu(obs_g), obs_o)
+    for t in range(6):
+        a = random_actions(rng, n)
+        if t == 2:
+            a[:64] = 0.0          # zero-tick cycles
+            a[64:128, 1] = 1.0    # longest coasts
+        r = env.step(torch.tensor(a), auto_reset=True)
+        ro = o.step(a, auto_reset=True)
+        assert np.array_equal(_cpu(r.obs), ro["obs"]), t
+        assert np.array_equal(_cpu(r.terminal_obs), ro["terminal_obs"]), t
+        assert np.array_equal(_cpu(r.reward), ro["reward"]), t
+        assert np.array_equal(_cpu(r.info), ro["info"]), t
+        assert np.array_equal(_cpu(r.terminated).astype(np.uint8), ro["terminated"]), t
+        assert np.array_equal(_cpu(r.truncated).astype(np.uint8), ro["truncated"]), t
+        assert_state_equal(env.get_state(), o.state, f"step {t}")
+
+
+def test_step_random_matches_oracle():
+    n = 2048
+    env, o = make_pair(n, seed=9)
+    o.reset()
+    rs = env.step_random(12)
+    rs_o, _ = o.step_random(12)
+    assert np.array_equal(_cpu(rs), rs_o)
+    assert_state_equal(env.get_state(), o.state, "step_random")
+
+
+def test_rollout_is_split_invariant_and_matches_oracle():
+    """Tick-budget rollouts: cutting the same work into different launches gives
+    identical bits, equal to the lock-step oracle at env-step boundaries, and
+    the rollout buffer holds the per-step outputs."""
+    n, steps = 1024, 6
+    p = default_params()
+    a = BatchedSalpEnv(n, params=p, seed=21)
+    b = BatchedSalpEnv(n, params=p, seed=21)
+    cap = steps
+    bufs = {"obs": torch.zeros((cap, n, 10), device="cuda"),
+            "actions": torch.zeros((cap, n, 3), device="cuda"),
+            "rewards": torch.zeros((cap, n), device="cuda"),
+            "dones": torch.zeros((cap, n), dtype=torch.uint8, device="cuda")}
+    sa = torch.zeros(n, dtype=torch.int64, device="cuda")
+    sb = torch.zeros(n, dtype=torch.int64, device="cuda")
+    a.rollout(10**7, buffers=bufs, steps_done=sa, max_steps=steps)
+    for _ in range(400):
+        b.rollout(97, steps_done=sb, max_steps=steps)
+        if int(sb.min()) >= steps:
+            break
+    assert int(sa.min()) == steps and int(sa.max()) == steps
+    assert int(sb.min()) == steps
+    ga, gb = _cpu(a.get_state()), _cpu(b.get_state())
+    assert np.array_equal(ga, gb)
+    o = orc.Oracle(p, n, seed=21)
+    o.reset()
+    # oracle step-by-step with the same Philox actions
+    from grasp_lab_salp_amd._abi import FIELD as FF
+    acts = []
+    outs = []
+    for t in range(steps):
+        act = np.zeros((n, 3), np.float32)
+        for i in range(n):
+            act[i] = philox_action(21, i, int(o.state[FF["step_count"], i]))
+        ro = o.step(act, auto_reset=True)
+        acts.append(act)
+        outs.append(ro)
+    assert_state_equal(ga, o.state, "rollout vs oracle")
+    for t in range(steps):
+        assert np.array_equal(_cpu(bufs["actions"][t]), acts[t])
+        assert np.array_equal(_cpu(bufs["obs"][t]), outs[t]["terminal_obs"])
+        assert np.array_equal(_cpu(bufs["rewards"][t]), outs[t]["reward"].astype(np.float32))
+        dn = outs[t]["terminated"] | (outs[t]["truncated"] << 1)
+        assert np.array_equal(_cpu(bufs["dones"][t]), dn)
+
+
+def philox_action(seed, env_id, step):
+    """sp_action() of salp_philox.h restated in Python for the test."""
+    out = orc.philox([step & 0xFFFFFFFF, step >> 32, env_id & 0xFFFFFFFF, 0 | ((env_id >> 32) << 1)],
+                     [seed & 0xFFFFFFFF, seed >> 32])
+    u = [np.float32(x >> 8) * np.float32(2.0 ** -24) for x in out[:3]]
+    return np.array([u[0], u[1], np.float32(2.0) * u[2] - np.float32(1.0)], np.float32)
+
+
+def test_sharding_by_env_id_offset():
+    """An env's trajectory depends only on its global id (multi-GPU sharding)."""
+    p = default_params()
+    full = BatchedSalpEnv(256, params=p, seed=4)
+    part = BatchedSalpEnv(64, params=p, seed=4, env_id_offset=128)
+    full.step_random(5)
+    part.step_random(5)
+    assert np.array_equal(_cpu(full.get_state())[:, 128:192], _cpu(part.get_state()))
+
+
+def test_timeout_and_zero_tick_cycles():
+    """500 zero-tick cycles (action [0,0,0]) truncate with the timeout penalty."""
+    n = 8
+    env, o = make_pair(n, seed=2)
+    o.reset()
+    a = np.zeros((n, 3), np.float32)
+    for t in range(500):
+        r = env.step(torch.tensor(a), auto_reset=False)
+    for t in range(500):
+        ro = o.step(a)
+    assert np.all(_cpu(r.truncated))
+    assert np.array_equal(_cpu(r.reward), ro["reward"])
+    assert_state_equal(env.get_state(), o.state, "timeout")
+    assert np.all(_cpu(env.field("cycle")) == 500)
+    assert np.all(_cpu(env.field("time")) == 0)
