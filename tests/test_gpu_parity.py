@@ -23,8 +23,8 @@ def _cpu(t):
 
 def assert_state_equal(gpu_state, cpu_state, what=""):
     g = _cpu(gpu_state) if torch.is_tensor(gpu_state) else gpu_state
-    bad = [(FIELDS[f], int(np.sum(g[f] != cpu_state[f]))) for f in range(NUM_FIELDS)
-           if not np.array_equal(g[f], cpu_state[f])]
+    bad = [(FIELDS[f], int(np.sum(~((g[f] == cpu_state[f]) | (np.isnan(g[f]) & np.isnan(cpu_state[f]))))))
+           for f in range(NUM_FIELDS) if not np.array_equal(g[f], cpu_state[f], equal_nan=True)]
     assert not bad, f"{what}: state fields differ from the oracle: {bad[:8]}"
 
 
@@ -58,7 +58,7 @@ def test_device_math_equals_oracle_math():
     ref = orc.math_selftest(x, y)
     g = _cpu(out)
     for r in range(9):
-        assert np.array_equal(g[r], ref[r]), f"math row {r}: {np.sum(g[r] != ref[r])} mismatches"
+        assert np.array_equal(g[r], ref[r], equal_nan=True), f"math row {r}: {np.sum(g[r] != ref[r])} mismatches"
 
 
 def test_fresh_envs_equal_oracle():
@@ -85,11 +85,11 @@ def test_teacher_forced_golden_rows(K):
     r = env.step(torch.tensor(d["action"][rows]), auto_reset=False)
     ro = o.step(d["action"][rows])
     assert_state_equal(env.get_state(), o.state, f"golden K={K}")
-    assert np.array_equal(_cpu(r.obs), ro["obs"])
-    assert np.array_equal(_cpu(r.reward), ro["reward"])
+    assert np.array_equal(_cpu(r.obs), ro["obs"], equal_nan=True)
+    assert np.array_equal(_cpu(r.reward), ro["reward"], equal_nan=True)
     assert np.array_equal(_cpu(r.terminated).astype(np.uint8), ro["terminated"])
     assert np.array_equal(_cpu(r.truncated).astype(np.uint8), ro["truncated"])
-    assert np.array_equal(_cpu(r.info), ro["info"])
+    assert np.array_equal(_cpu(r.info), ro["info"], equal_nan=True)
     # and directly against the reference itself (same tolerances as the oracle tests)
     after = snapshot_to_state(d, "a_", rows)
     g = _cpu(env.get_state())
@@ -121,10 +121,10 @@ def test_random_batch_free_running_with_auto_reset():
             a[64:128, 1] = 1.0    # longest coasts
         r = env.step(torch.tensor(a), auto_reset=True)
         ro = o.step(a, auto_reset=True)
-        assert np.array_equal(_cpu(r.obs), ro["obs"]), t
-        assert np.array_equal(_cpu(r.terminal_obs), ro["terminal_obs"]), t
-        assert np.array_equal(_cpu(r.reward), ro["reward"]), t
-        assert np.array_equal(_cpu(r.info), ro["info"]), t
+        assert np.array_equal(_cpu(r.obs), ro["obs"], equal_nan=True), t
+        assert np.array_equal(_cpu(r.terminal_obs), ro["terminal_obs"], equal_nan=True), t
+        assert np.array_equal(_cpu(r.reward), ro["reward"], equal_nan=True), t
+        assert np.array_equal(_cpu(r.info), ro["info"], equal_nan=True), t
         assert np.array_equal(_cpu(r.terminated).astype(np.uint8), ro["terminated"]), t
         assert np.array_equal(_cpu(r.truncated).astype(np.uint8), ro["truncated"]), t
         assert_state_equal(env.get_state(), o.state, f"step {t}")
@@ -136,7 +136,7 @@ def test_step_random_matches_oracle():
     o.reset()
     rs = env.step_random(12)
     rs_o, _ = o.step_random(12)
-    assert np.array_equal(_cpu(rs), rs_o)
+    assert np.array_equal(_cpu(rs), rs_o, equal_nan=True)
     assert_state_equal(env.get_state(), o.state, "step_random")
 
 
@@ -163,7 +163,7 @@ def test_rollout_is_split_invariant_and_matches_oracle():
     assert int(sa.min()) == steps and int(sa.max()) == steps
     assert int(sb.min()) == steps
     ga, gb = _cpu(a.get_state()), _cpu(b.get_state())
-    assert np.array_equal(ga, gb)
+    assert np.array_equal(ga, gb, equal_nan=True)
     o = orc.Oracle(p, n, seed=21)
     o.reset()
     # oracle step-by-step with the same Philox actions
@@ -180,8 +180,8 @@ def test_rollout_is_split_invariant_and_matches_oracle():
     assert_state_equal(ga, o.state, "rollout vs oracle")
     for t in range(steps):
         assert np.array_equal(_cpu(bufs["actions"][t]), acts[t])
-        assert np.array_equal(_cpu(bufs["obs"][t]), outs[t]["terminal_obs"])
-        assert np.array_equal(_cpu(bufs["rewards"][t]), outs[t]["reward"].astype(np.float32))
+        assert np.array_equal(_cpu(bufs["obs"][t]), outs[t]["terminal_obs"], equal_nan=True)
+        assert np.array_equal(_cpu(bufs["rewards"][t]), outs[t]["reward"].astype(np.float32), equal_nan=True)
         dn = outs[t]["terminated"] | (outs[t]["truncated"] << 1)
         assert np.array_equal(_cpu(bufs["dones"][t]), dn)
 
@@ -201,7 +201,24 @@ def test_sharding_by_env_id_offset():
     part = BatchedSalpEnv(64, params=p, seed=4, env_id_offset=128)
     full.step_random(5)
     part.step_random(5)
-    assert np.array_equal(_cpu(full.get_state())[:, 128:192], _cpu(part.get_state()))
+    assert np.array_equal(_cpu(full.get_state())[:, 128:192], _cpu(part.get_state()), equal_nan=True)
+
+
+def test_reference_blowup_is_reproduced():
+    """The reference's explicit integrator diverges when jet_time < dt (e.g. the
+    action below: refill 0.0074 s, jet 0.0060 s): velocities overflow and turn
+    NaN at tick 100 of the cycle (checked against the Python reference, see
+    DESIGN.md).  The device reproduces it exactly as the oracle does."""
+    env, o = make_pair(4, seed=0)
+    o.reset()
+    env.set_state(torch.tensor(o.state))
+    a = np.tile(np.float32([0.0904393, 0.06936062, -0.76570743]), (4, 1))
+    r = env.step(torch.tensor(a))
+    ro = o.step(a)
+    assert ro["ticks"][0] == 151
+    assert np.all(np.isnan(ro["obs"][:, :6]))
+    assert np.array_equal(_cpu(r.obs), ro["obs"], equal_nan=True)
+    assert_state_equal(env.get_state(), o.state, "blow-up")
 
 
 def test_timeout_and_zero_tick_cycles():
@@ -215,7 +232,7 @@ def test_timeout_and_zero_tick_cycles():
     for t in range(500):
         ro = o.step(a)
     assert np.all(_cpu(r.truncated))
-    assert np.array_equal(_cpu(r.reward), ro["reward"])
+    assert np.array_equal(_cpu(r.reward), ro["reward"], equal_nan=True)
     assert_state_equal(env.get_state(), o.state, "timeout")
     assert np.all(_cpu(env.field("cycle")) == 500)
     assert np.all(_cpu(env.field("time")) == 0)
