@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--n-envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--tick-budget", type=int, default=8192, help="physics ticks per env per launch")
     ap.add_argument("--capacity", type=int, default=16, help="rollout-buffer slots per env")
+    ap.add_argument("--chunk", type=int, default=32, help="ticks between env-step boundaries")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -97,7 +98,7 @@ def main():
             dist.barrier()
 
     for _ in range(a.warmup):
-        env.rollout(a.tick_budget, buffers=bufs, steps_done=done)
+        env.rollout(a.tick_budget, buffers=bufs, steps_done=done, chunk=a.chunk)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -107,7 +108,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(a.steps):
         starts[k].record()
-        env.rollout(a.tick_budget, buffers=bufs, steps_done=done)
+        env.rollout(a.tick_budget, buffers=bufs, steps_done=done, chunk=a.chunk)
         ends[k].record()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -141,7 +142,7 @@ def main():
         dist.destroy_process_group()
         return
 
-    ticks_total = float(a.tick_budget) * n * a.steps * world
+    ticks_total = float(-(-a.tick_budget // a.chunk) * a.chunk) * n * a.steps * world
     steps_per_launch = steps_local / a.steps
     bytes_launch = n * (2 * STATE_BYTES + 16) + steps_per_launch * STEP_OUT_BYTES
     achieved = bytes_launch / (kern_ms / 1e3) / 1e9
@@ -160,7 +161,7 @@ def main():
         "data": "synthetic: Philox U(action box) actions, Philox targets/obstacles on auto-reset",
         "config": {"workload": "65536 envs/GPU random-action chained rollout + rollout-buffer fill, "
                                "canonical make_env robot (src/train_robot.py:11-21), 2 obstacles",
-                   "n_envs_per_gpu": n, "tick_budget": a.tick_budget, "rollout_capacity": cap,
+                   "n_envs_per_gpu": n, "tick_budget": a.tick_budget, "chunk": a.chunk, "rollout_capacity": cap,
                    "parallelism": f"env-shard x{world}"},
         "ticks_per_sec": ticks_total / elapsed,
         "mean_ticks_per_env_step": ticks_total / max(steps_total, 1.0),

@@ -28,6 +28,8 @@ class SalpRolloutBuffers(ctypes.Structure):
         ("dones", ctypes.c_void_p),
         ("steps_done", ctypes.c_void_p),
         ("max_steps", ctypes.c_int64),
+        ("chunk", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
     ]
 
 

@@ -150,7 +150,7 @@ class BatchedSalpEnv:
         self._check(_lib.load().salp_step_random(self._h, int(n_steps), _ptr(rs), self._stream()))
         return rs
 
-    def rollout(self, tick_budget, buffers=None, steps_done=None, max_steps=0):
+    def rollout(self, tick_budget, buffers=None, steps_done=None, max_steps=0, chunk=32):
         """Chained random-action rollout: each env runs ``tick_budget`` physics
         ticks, completing as many env-steps as fit (auto-reset).  ``buffers`` is
         an optional dict of preallocated device tensors {obs [cap,n,obs_dim],
@@ -174,6 +174,7 @@ class BatchedSalpEnv:
                 raise ValueError("steps_done must be an int64 tensor with n_envs elements")
             B.steps_done = steps_done.data_ptr()
         B.max_steps = int(max_steps)
+        B.chunk = int(chunk)
         self._check(_lib.load().salp_rollout(self._h, int(tick_budget), ctypes.byref(B), self._stream()))
         return steps_done
 

@@ -114,23 +114,23 @@ __global__ __launch_bounds__(kBlock) void k_step_random(double* S, Params P, int
     salp::store_hot(h, S, P, i);
 }
 
-// Chained random-action rollout under a per-lane tick budget, filling the
-// rollout buffer.  A lane finishes the env-step whose cycle ends, immediately
-// starts the next one, and never idles while other lanes of its wave are still
-// inside a long cycle.
-__global__ __launch_bounds__(kBlock) void k_rollout(double* S, Params P, int64_t tick_budget,
-                                                    int64_t max_steps, SalpRolloutBuffers B) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P.n) return;
-    Hot h;
-    salp::load_hot(h, S, P, i);
-    const uint64_t env_id = (uint64_t)(P.env_offset + i);
-    bool pending = SF(SALP_F_PENDING) != 0.0;
-    if (pending) salp::resume_cycle(h, S, P, i);
-    int64_t steps = B.steps_done ? B.steps_done[i] : 0;
-    int64_t ticks = 0, events = 0;
-    for (;;) {
-        if (pending && !(h.ct < h.b2)) {
+// Chained random-action rollout, filling the rollout buffer.  Work proceeds in
+// chunks of `chunk` physics ticks: inside a chunk every lane whose cycle is
+// still running ticks (a tight loop over salp::tick only); between chunks the
+// lanes whose cycle ended finish that env-step and start the next one
+// together, so the heavy env-step epilogue runs once per chunk for all lanes
+// that need it instead of once per lane.  A lane idles at most `chunk` ticks
+// per env-step.  Per-env results depend only on (seed, env id): how the work
+// is cut into launches and chunks changes nothing but the count of env-steps
+// a launch completes.
+__device__ __forceinline__ void rollout_boundary(Hot& h, double* S, const Params& P, int64_t i,
+                                                 uint64_t env_id, bool& pending, bool& active,
+                                                 int64_t& steps, int64_t max_steps,
+                                                 const SalpRolloutBuffers& B) {
+    // a few rounds so that zero-tick cycles chain without waiting a chunk
+    for (int rep = 0; rep < 4; ++rep) {
+        const bool fin = active && pending && !(h.ct < h.b2);
+        if (fin) {
             SF(SALP_F_STEP_COUNT) = SF(SALP_F_STEP_COUNT) + 1.0;
             float o[SALP_OBS_DIM_MAX];
             salp::StepOut r = salp::finish_step(h, S, P, i, o, nullptr);
@@ -148,22 +148,39 @@ __global__ __launch_bounds__(kBlock) void k_rollout(double* S, Params P, int64_t
                 if (B.dones) B.dones[row] = (uint8_t)((r.terminated ? 1 : 0) | (r.truncated ? 2 : 0));
             }
             ++steps;
-            ++events;
             pending = false;
             if (r.terminated || r.truncated) salp::reset_env_philox(h, S, P, i, nullptr);
+            if (max_steps > 0 && steps >= max_steps) active = false;
         }
-        if (!pending) {
-            if ((max_steps > 0 && steps >= max_steps) || events > tick_budget) break;
+        const bool beg = active && !pending;
+        if (beg) {
             float a[3];
             sp_action(P.seed, env_id, (uint64_t)SF(SALP_F_STEP_COUNT), a);
             salp::begin_step(h, S, P, i, a[0], a[1], a[2]);
             pending = true;
-            continue;
         }
-        if (ticks >= tick_budget) break;
-        salp::tick(h, P);
-        ++ticks;
+        if (!fin && !beg) break;
     }
+}
+
+__global__ __launch_bounds__(kBlock) void k_rollout(double* S, Params P, int64_t n_chunks,
+                                                    int32_t chunk, int64_t max_steps,
+                                                    SalpRolloutBuffers B) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    Hot h;
+    salp::load_hot(h, S, P, i);
+    const uint64_t env_id = (uint64_t)(P.env_offset + i);
+    bool pending = SF(SALP_F_PENDING) != 0.0;
+    if (pending) salp::resume_cycle(h, S, P, i);
+    int64_t steps = B.steps_done ? B.steps_done[i] : 0;
+    bool active = !(max_steps > 0 && steps >= max_steps);
+    for (int64_t c = 0; c < n_chunks; ++c) {
+        rollout_boundary(h, S, P, i, env_id, pending, active, steps, max_steps, B);
+        for (int32_t k = 0; k < chunk; ++k)
+            if (active && h.ct < h.b2) salp::tick(h, P);
+    }
+    rollout_boundary(h, S, P, i, env_id, pending, active, steps, max_steps, B);
     if (B.steps_done) B.steps_done[i] = steps;
     salp::store_hot(h, S, P, i);
 }
@@ -377,8 +394,10 @@ int salp_rollout(SalpEnv* h, int64_t tick_budget, const SalpRolloutBuffers* buf,
     SalpRolloutBuffers b{};
     if (buf) b = *buf;
     if (b.capacity < 0) return fail(h, SALP_EINVAL, "salp_rollout: capacity < 0");
+    int32_t chunk = b.chunk > 0 ? b.chunk : 32;
+    int64_t n_chunks = (tick_budget + chunk - 1) / chunk;
     hipLaunchKernelGGL(k_rollout, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream,
-                       h->state, h->dp, tick_budget, b.max_steps, b);
+                       h->state, h->dp, n_chunks, chunk, b.max_steps, b);
     return launched(h, "k_rollout");
 }
 

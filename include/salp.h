@@ -92,6 +92,8 @@ typedef struct SalpRolloutBuffers {
     int64_t* steps_done;   /* [n_envs] completed env-steps counter (in/out)    */
     int64_t max_steps;     /* >0: a lane starts no env-step once steps_done
                             * reaches it (fixed-length rollouts, n_steps)     */
+    int32_t chunk;         /* ticks between env-step boundaries (0 = 32)      */
+    int32_t reserved;
 } SalpRolloutBuffers;
 
 /* ------------------------------------------------------------ lifecycle */
@@ -122,11 +124,13 @@ int salp_reset_to(SalpEnv* h, const uint8_t* mask, const float* targets, const f
 int salp_step(SalpEnv* h, const float* actions, float* obs_out, double* reward_out,
               uint8_t* terminated_out, uint8_t* truncated_out, int auto_reset,
               float* terminal_obs_out, double* info_out, void* stream);
-/* Synthetic random-action rollout, chained per lane: every env runs exactly
- * `tick_budget` physics ticks (dt=0.01 each), completing as many env-steps as
- * fit, with actions ~ U(action box) from Philox(seed; env id, step index) and
- * auto-reset (Philox targets/obstacles).  A cycle cut by the budget resumes
- * on the next call; results do not depend on how ticks are split. */
+/* Synthetic random-action rollout, chained per lane: every env runs up to
+ * `tick_budget` physics ticks (dt=0.01 each) in chunks of buf->chunk ticks,
+ * completing as many env-steps as fit, with actions ~ U(action box) from
+ * Philox(seed; env id, step index) and auto-reset (Philox targets/obstacles).
+ * Env-steps end and start only at chunk boundaries (a lane waits < chunk
+ * ticks); a cycle cut by the budget resumes on the next call.  Per-env results
+ * do not depend on how the work is split. */
 int salp_rollout(SalpEnv* h, int64_t tick_budget, const SalpRolloutBuffers* buf, void* stream);
 /* Same random actions, lock-step: every env performs exactly n_steps
  * env-steps (one full cycle each) with auto-reset.  rewards_out [n] = sum. */
