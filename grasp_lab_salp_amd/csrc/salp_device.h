@@ -89,11 +89,7 @@ SD float cubef(float x) {
 /* Rotation R = Rz(psi) Ry(theta) Rx(phi) (src/dynamics.py:34-58) from the
  * dgemm-order product with its zeros removed. */
 struct Rot { double r[3][3]; };
-SD Rot rot_zyx(double phi, double theta, double psi) {
-    double sp, cp, st, ct, ss, cs;
-    sm_sincos(phi, &sp, &cp);
-    sm_sincos(theta, &st, &ct);
-    sm_sincos(psi, &ss, &cs);
+SD Rot rot_sc(double sp, double cp, double st, double ct, double ss, double cs) {
     /* A = Rz @ Ry */
     double a00 = cs * ct, a01 = -ss, a02 = cs * st;
     double a10 = ss * ct, a11 = cs, a12 = ss * st;
@@ -103,6 +99,13 @@ SD Rot rot_zyx(double phi, double theta, double psi) {
     R.r[1][0] = a10; R.r[1][1] = sm_fma(a12, sp, a11 * cp); R.r[1][2] = sm_fma(a12, cp, a11 * -sp);
     R.r[2][0] = a20; R.r[2][1] = a22 * sp;                   R.r[2][2] = a22 * cp;
     return R;
+}
+SD Rot rot_zyx(double phi, double theta, double psi) {
+    double sp, cp, st, ct, ss, cs;
+    sm_sincos(phi, &sp, &cp);
+    sm_sincos(theta, &st, &ct);
+    sm_sincos(psi, &ss, &cs);
+    return rot_sc(sp, cp, st, ct, ss, cs);
 }
 /* R @ v (dgemv order) */
 SD void rot_apply(const Rot& R, double v0, double v1, double v2, double* o) {
@@ -115,132 +118,136 @@ SD void rot_body_xy(const Rot& R, double d0, double d1, double* b0, double* b1) 
 }
 
 /* ---------------------------------------------- geometry (src/geometry.py) */
-/* body geometry derived from (length, width, volume, prev volume) */
-struct Geo {
-    double A0, A1;           /* cross-sectional areas yz, xz(=xy) */
-    double wm, m, mr;        /* water mass, total mass, mass rate */
-    double nr;               /* drag-coefficient interpolation ratio (clipped) */
-    double I0, I1;           /* inertia diag xx, yy(=zz) */
-};
+/* NumPy 2 performs some geometry operations in float32 (see the file header).
+ * Both dtypes run through ONE branch-free code path: every operation is done
+ * in fp64 and, in float32 mode, rounded to float32 right after (r32).  For
+ * float32 operands this equals the float32 operation exactly (double rounding
+ * is innocuous for + - * / sqrt when the wide format has >= 2p+2 bits, 53 >=
+ * 50).  Constants that NumPy converts to float32 are selected per lane (sel).
+ * No lane-divergent branch, so a wave never executes both dtype variants. */
+SD double r32(double x, bool f) { return f ? (double)(float)x : x; }
+SD double sel(bool f, double c) { return f ? (double)(float)c : c; }
 
-/* compute_water_volume_jit (src/geometry.py:78-81) */
-SD double ellipsoid_volume(double L, double W, bool f32) {
-    if (f32) {
-        float lh = (float)L / 2.0f, wh = (float)W / 2.0f;
-        return (double)((float)((4.0 / 3.0) * PI) * lh * sqf(wh));
-    }
-    double wh = W / 2.0;
-    return (4.0 / 3.0) * PI * (L / 2.0) * (wh * wh);
+/* f32 / f64 x**3 (NumPy: float32 ** 3 -> powf, float64 ** 3 -> pow; both
+ * correctly rounded here).  For float32 x the double-double cube (h, lo) is
+ * exact and rounding h to float32 only needs fixing when h is a float32 tie. */
+SD double cube_sel(double x, bool f) {
+    double p = x * x, pe = sm_fma(x, x, -p);
+    double h = p * x, he = sm_fma(p, x, -h);
+    double lo = sm_fma(pe, x, he);
+    double c64 = h + lo;
+    float r = (float)h;
+    double d = h - (double)r;
+    float nb = nextafterf(r, d > 0 ? INFINITY : -INFINITY);
+    double ulp = (double)nb - (double)r;
+    bool tie = d != 0.0 && fabs(d) * 2.0 == fabs(ulp) && lo != 0.0;
+    float r2 = (tie && ((lo > 0) == (d > 0))) ? nb : r;
+    return f ? (double)r2 : c64;
+}
+
+/* Shared pieces of compute_water_volume_jit / compute_inertia_matrix_jit /
+ * compute_center_of_mass_jit for one (length, width) */
+struct Core {
+    double lh, wh, lh2, wh2, t;   /* L/2, W/2, (L/2)^2, (W/2)^2, L/2 - 0.08 */
+    double vell, wme;             /* ellipsoid water volume, 1000 * vell */
+};
+SD Core core(double L, double W, bool f) {
+    Core c;
+    c.lh = L / 2.0;
+    c.wh = W / 2.0;
+    c.lh2 = r32(c.lh * c.lh, f);
+    c.wh2 = r32(c.wh * c.wh, f);
+    c.t = r32(c.lh - sel(f, 0.08), f);
+    c.vell = r32(r32(sel(f, (4.0 / 3.0) * PI) * c.lh, f) * c.wh2, f);   /* src/geometry.py:78-81 */
+    c.wme = r32(1000.0 * c.vell, f);
+    return c;
 }
 /* Robot._get_water_volume (src/robot.py:1055-1056) */
-SD double water_volume(const Params& P, double L, double W, bool f32) {
-    if (f32) return (double)((float)ellipsoid_volume(L, W, true) - (float)P.tube_volume);
-    return ellipsoid_volume(L, W, false) - P.tube_volume;
+SD double water_volume(const Params& P, const Core& c, bool f) {
+    return r32(c.vell - sel(f, P.tube_volume), f);
 }
 /* water mass = density * volume (src/robot.py:1058-1063) */
-SD double water_mass(const Params& P, double V, bool f32) {
-    return f32 ? (double)((float)P.density * (float)V) : P.density * V;
-}
-
-SD Geo geometry(const Params& P, double L, double W, double V, double pV, bool g32, bool pv32) {
-    Geo g;
-    /* compute_cross_sectional_area_jit (src/geometry.py:67-75) */
-    if (g32) {
-        float wh = (float)W / 2.0f, lh = (float)L / 2.0f, pi = (float)PI;
-        g.A0 = (double)(pi * wh * wh);
-        g.A1 = (double)(pi * lh * wh);
-    } else {
-        double wh = W / 2.0, lh = L / 2.0;
-        g.A0 = PI * wh * wh;
-        g.A1 = PI * lh * wh;
-    }
-    /* get_mass / get_mass_rate (src/robot.py:1061-1066, 651-654) */
-    g.wm = water_mass(P, V, g32);
-    double pwm = pv32 ? (double)((float)pV * (float)P.density) : pV * P.density;
-    if (g32) {
-        g.m = (double)((float)P.dry_mass + (float)g.wm + (float)P.nozzle_mass);
-    } else {
-        g.m = P.dry_mass + g.wm + P.nozzle_mass;
-    }
-    if (g32 && pv32) g.mr = (double)(((float)g.wm - (float)pwm) / (float)DT);
-    else g.mr = (g.wm - pwm) / DT;
-    /* compute_drag_coefficient_jit (src/geometry.py:104-123) */
-    double nr;
-    if (g32) {
-        float aspect = (float)L / (float)W;
-        nr = (double)((aspect - (float)P.end_aspect) / (float)P.aspect_den);
-    } else {
-        nr = (L / W - P.end_aspect) / P.aspect_den;
-    }
-    if (nr < 0.0) nr = 0.0;
-    if (nr > 1.0) nr = 1.0;
-    g.nr = nr;
-    /* compute_inertia_matrix_jit (src/geometry.py:133-183) */
-    if (g32) {
-        float lh = (float)L / 2.0f, wh = (float)W / 2.0f;
-        float lh2 = sqf(lh), wh2 = sqf(wh);
-        float t8 = sqf(lh - 0.08f), n25 = sqf(lh + 0.025f);
-        float p1 = (float)(1.0 / 3.0 * SKIN_MASS);
-        float k = 0.2f * (1000.0f * (float)ellipsoid_volume(L, W, true));
-        float sxx = p1 * (wh2 + wh2), syy = p1 * (lh2 + wh2);
-        float wxx = k * (wh2 + wh2), wyy = k * (lh2 + wh2);
-        g.I0 = (double)sxx + (double)wxx;
-        g.I1 = BUOY_MASS * (double)lh2 + P.net_tube_mass * (double)t8 + (double)syy + (double)wyy +
-               P.nozzle_mass * (double)n25;
-    } else {
-        double lh = L / 2.0, wh = W / 2.0;
-        double lh2 = lh * lh, wh2 = wh * wh;
-        double t8 = lh - 0.08, n25 = lh + 0.025;
-        double p1 = 1.0 / 3.0 * SKIN_MASS;
-        double k = 0.2 * (1000.0 * ellipsoid_volume(L, W, false));
-        g.I0 = p1 * (wh2 + wh2) + k * (wh2 + wh2);
-        g.I1 = BUOY_MASS * lh2 + P.net_tube_mass * (t8 * t8) + p1 * (lh2 + wh2) + k * (lh2 + wh2) +
-               P.nozzle_mass * (n25 * n25);
-    }
-    return g;
-}
+SD double water_mass(const Params& P, double V, bool f) { return r32(sel(f, P.density) * V, f); }
 
 /* compute_center_of_mass_jit (src/geometry.py:186-203), x component */
-SD double center_of_mass(const Params& P, double L, double W, double wm, bool f32) {
-    if (f32) {
-        float Lf = (float)L;
-        float pbx = Lf / 2.0f, ptx = Lf / 2.0f - 0.08f, pnx = -Lf / 2.0f - 0.025f + 0.05f;
-        float wme = 1000.0f * (float)ellipsoid_volume(L, W, true);
-        double num = (double)wme * 0.0 - P.P1000tv * (double)ptx;
-        float den = wme - (float)P.P1000tv;
-        double pwx = num / (double)den;
-        float total = (float)P.com_mass_sum + (float)wm;
-        return (TUBE_MASS * (double)ptx + P.nozzle_mass * (double)pnx + BUOY_MASS * (double)pbx +
-                SKIN_MASS * 0.0 + wm * pwx) / (double)total;
-    }
-    double pbx = L / 2, ptx = L / 2 - 0.08, pnx = -L / 2 - 0.025 + 0.05;
-    double wme = 1000.0 * ellipsoid_volume(L, W, false);
-    double pwx = (wme * 0.0 - P.P1000tv * ptx) / (wme - P.P1000tv);
-    double total = P.com_mass_sum + wm;
+SD double center_of_mass(const Params& P, const Core& c, double wm, bool f) {
+    double pbx = c.lh, ptx = c.t;
+    double pnx = r32(r32(-c.lh - sel(f, 0.025), f) + sel(f, 0.05), f);
+    double num = c.wme * 0.0 - P.P1000tv * ptx;
+    double den = r32(c.wme - sel(f, P.P1000tv), f);
+    double pwx = num / den;
+    double total = r32(sel(f, P.com_mass_sum) + wm, f);
     return (TUBE_MASS * ptx + P.nozzle_mass * pnx + BUOY_MASS * pbx + SKIN_MASS * 0.0 + wm * pwx) /
            total;
 }
 
-/* compute_length_jit / compute_width_jit (src/geometry.py:39-64) */
-SD double body_length(const Params& P, int st, double ct, double refill, double mx, double c,
-                      double cr, double rr, bool* f32) {
-    *f32 = false;
-    if (st == REFILL) {
-        if (ct < refill) return P.L0 - ct * cr;
-        *f32 = true;
-        return (double)((float)P.L0 - (float)c);
-    }
-    if (st == JET) return (double)((float)P.L0 - (float)c) + (ct - mx) * rr;
-    return P.L0;
+/* Everything the next tick's dynamics needs from (length, width, volume,
+ * prev volume): computed once in update_properties and carried in registers. */
+struct Geo {
+    double m, mr;                 /* total mass, water-mass rate */
+    double I0, I1;                /* inertia diag xx, yy (= zz) */
+    double kc0, kc1;              /* drag force: (-0.5 rho A) * C_t per axis (y = z) */
+    double ra0, ra1;              /* drag torque: C_r * (-0.5 rho) * A per axis (y = z) */
+    double dimx, dimy;            /* width**3, length**3 */
+    double speed;                 /* jet speed (V - V_prev) / dt / A_nozzle */
+    double rx;                    /* jet moment arm x */
+};
+SD Geo make_geo(const Params& P, const Core& c, double L, double W, double V, double pV, bool g32,
+                bool pv32, double wm) {
+    Geo g;
+    const bool f = g32, b32 = g32 && pv32;
+    /* get_mass / get_mass_rate (src/robot.py:1061-1066, 651-654); wm = water mass */
+    double pwm = r32(sel(pv32, P.density) * pV, pv32);
+    g.m = r32(r32(sel(f, P.dry_mass) + wm, f) + sel(f, P.nozzle_mass), f);
+    g.mr = r32(r32(wm - pwm, b32) / sel(b32, DT), b32);
+    /* compute_cross_sectional_area_jit (src/geometry.py:67-75) */
+    double pi = sel(f, PI);
+    double A0 = r32(r32(pi * c.wh, f) * c.wh, f);
+    double A1 = r32(r32(pi * c.lh, f) * c.wh, f);
+    /* compute_drag_coefficient_jit (src/geometry.py:104-123) */
+    double aspect = r32(L / W, f);
+    double nr = r32(r32(aspect - sel(f, P.end_aspect), f) / sel(f, P.aspect_den), f);
+    nr = nr < 0.0 ? 0.0 : nr;
+    nr = nr > 1.0 ? 1.0 : nr;
+    /* compute_drag_force_jit / compute_drag_torque_jit coefficients
+     * (src/dynamics.py:110-128; ranges src/robot.py:415-434) */
+    const double k = -0.5 * P.density;
+    double tcd0 = 2.5 - nr * (2.5 - 1.5), tcd1 = 1.5 - nr * (1.5 - 2.5);
+    double rcd0 = 0.3 - nr * (0.3 - 0.1), rcd1 = 0.2 - nr * (0.2 - 0.5);
+    g.kc0 = r32(A0 * k, f) * tcd0;
+    g.kc1 = r32(A1 * k, f) * tcd1;
+    g.ra0 = rcd0 * k * A0;
+    g.ra1 = rcd1 * k * A1;
+    g.dimx = cube_sel(W, f);
+    g.dimy = cube_sel(L, f);
+    /* compute_inertia_matrix_jit (src/geometry.py:133-183) */
+    double p1 = sel(f, 1.0 / 3.0 * SKIN_MASS);
+    double sx = r32(c.wh2 + c.wh2, f), sy = r32(c.lh2 + c.wh2, f);
+    double kw = r32(sel(f, 0.2) * c.wme, f);
+    double t8 = r32(c.t * c.t, f);
+    double n = r32(c.lh + sel(f, 0.025), f);
+    double n25 = r32(n * n, f);
+    g.I0 = r32(p1 * sx, f) + r32(kw * sx, f);
+    g.I1 = BUOY_MASS * c.lh2 + P.net_tube_mass * t8 + r32(p1 * sy, f) + r32(kw * sy, f) +
+           P.nozzle_mass * n25;
+    /* compute_jet_velocity_jit speed (src/dynamics.py:87-94) */
+    g.speed = r32(r32(r32(V - pV, b32) / sel(b32, DT), b32) / sel(b32, P.nozzle_area), b32);
+    /* compute_jet_moment_arm_jit (src/geometry.py:126-130) */
+    g.rx = P.mid_x + -L / 2.0;
+    return g;
 }
-SD double body_width(const Params& P, int st, double ct, double refill, double mx, double c,
-                     double cr, double rr) {
-    if (st == REFILL) {
-        if (ct < refill) return P.W0 + ct * cr;
-        return (double)((float)P.W0 + (float)c);
-    }
-    if (st == JET) return (double)((float)P.W0 + (float)c) - (ct - mx) * rr;
-    return P.W0;
+
+/* compute_length_jit / compute_width_jit (src/geometry.py:39-64); in REFILL
+ * past refill_time both are np.float32 (`init_length - contraction`), in JET
+ * that float32 difference is the first operand of a float64 sum. */
+SD void body_lw(const Params& P, int phase, double ct, double refill, double mx, double c,
+                double cr, double rr, double* L, double* W, bool* f32) {
+    const bool fill = phase == REFILL, jet = phase == JET, early = ct < refill;
+    const double Lc = (double)((float)P.L0 - (float)c), Wc = (double)((float)P.W0 + (float)c);
+    const double x = (ct - mx) * rr;
+    *L = fill ? (early ? P.L0 - ct * cr : Lc) : (jet ? Lc + x : P.L0);
+    *W = fill ? (early ? P.W0 + ct * cr : Wc) : (jet ? Wc - x : P.W0);
+    *f32 = fill && !early;
 }
 
 /* ---------------------------------------------------- per-lane state */
@@ -252,11 +259,22 @@ struct Hot {
     double refill, jet, coast, c, cr, rr, turn;                /* cycle constants */
     double mx, b1, b2;                                         /* phase boundaries */
     double d0, d1, d2;                                         /* nozzle direction */
+    double sp, cp, st, cth;                                    /* sin/cos of roll, pitch */
+    Geo geo;                                                   /* geometry of (L, W, V, pV) */
     int phase;
     bool g32, pv32;
 };
 
 #define SF(f) S[(size_t)(f) * (size_t)P.n + (size_t)i]
+
+/* Register-resident values derived from the stored state: geometry of the
+ * current body and sin/cos of roll and pitch. */
+SD void refresh_derived(Hot& h, const Params& P) {
+    const Core c = core(h.L, h.W, h.g32);
+    h.geo = make_geo(P, c, h.L, h.W, h.V, h.pV, h.g32, h.pv32, water_mass(P, h.V, h.g32));
+    sm_sincos(h.e0, &h.sp, &h.cp);
+    sm_sincos(h.e1, &h.st, &h.cth);
+}
 
 SD void load_hot(Hot& h, const double* S, const Params& P, int64_t i) {
     h.v0 = SF(SALP_F_V0); h.v1 = SF(SALP_F_V1); h.v2 = SF(SALP_F_V2);
@@ -277,6 +295,7 @@ SD void load_hot(Hot& h, const double* S, const Params& P, int64_t i) {
     h.c = SF(SALP_F_CONTRACTION); h.cr = SF(SALP_F_CONTRACT_RATE); h.rr = SF(SALP_F_RELEASE_RATE);
     h.turn = SF(SALP_F_TURN_TIME);
     h.phase = (int)SF(SALP_F_PHASE);
+    refresh_derived(h, P);
 }
 SD void store_hot(const Hot& h, double* S, const Params& P, int64_t i) {
     SF(SALP_F_V0) = h.v0; SF(SALP_F_V1) = h.v1; SF(SALP_F_V2) = h.v2;
@@ -330,9 +349,8 @@ SD void cycle_bounds(Hot& h) {
  * _update_motion_states (:860-875); then cycle_time, update_state,
  * update_properties (:640-668). */
 SD void tick(Hot& h, const Params& P) {
-    const Geo g = geometry(P, h.L, h.W, h.V, h.pV, h.g32, h.pv32);
+    const Geo& g = h.geo;
     const double m = g.m;
-    const double k = -0.5 * P.density;
     /* ---------------- Newton ---------------- */
     /* Coriolis force -w x (M v)  (src/dynamics.py:159-162) */
     double mv0 = m * h.v0, mv1 = m * h.v1, mv2 = m * h.v2;
@@ -340,28 +358,14 @@ SD void tick(Hot& h, const Params& P) {
            cf2 = -(h.w0 * mv1 - h.w1 * mv0);
     /* drag force (src/dynamics.py:110-116) */
     double vn = np_norm3(h.v0, h.v1, h.v2);
-    double tcd0 = 2.5 - g.nr * (2.5 - 1.5), tcd1 = 1.5 - g.nr * (1.5 - 2.5);
-    double ka0, ka1;
-    if (h.g32) { ka0 = (double)((float)k * (float)g.A0); ka1 = (double)((float)k * (float)g.A1); }
-    else { ka0 = g.A0 * k; ka1 = g.A1 * k; }
-    double kc0 = ka0 * tcd0, kc1 = ka1 * tcd1;
-    double df0 = kc0 * vn * h.v0 + kc0 * h.v0 * DRAG_FORCE_RATIO;
-    double df1 = kc1 * vn * h.v1 + kc1 * h.v1 * DRAG_FORCE_RATIO;
-    double df2 = kc1 * vn * h.v2 + kc1 * h.v2 * DRAG_FORCE_RATIO;
-    /* jet force (src/robot.py:937-951, src/dynamics.py:87-101) */
-    double jf0 = 0.0, jf1 = 0.0, jf2 = 0.0;
-    if (h.phase == JET) {
-        double speed;
-        if (h.g32 && h.pv32) {
-            float vr = ((float)h.V - (float)h.pV) / (float)DT;
-            speed = (double)(vr / (float)P.nozzle_area);
-        } else {
-            speed = ((h.V - h.pV) / DT) / P.nozzle_area;
-        }
-        jf0 = g.mr * (h.d0 * speed) * -CD;
-        jf1 = g.mr * (h.d1 * speed) * -CD;
-        jf2 = g.mr * (h.d2 * speed) * -CD;
-    }
+    double df0 = g.kc0 * vn * h.v0 + g.kc0 * h.v0 * DRAG_FORCE_RATIO;
+    double df1 = g.kc1 * vn * h.v1 + g.kc1 * h.v1 * DRAG_FORCE_RATIO;
+    double df2 = g.kc1 * vn * h.v2 + g.kc1 * h.v2 * DRAG_FORCE_RATIO;
+    /* jet force, JET phase only (src/robot.py:937-951, src/dynamics.py:87-101) */
+    const bool jet = h.phase == JET;
+    double jf0 = jet ? g.mr * (h.d0 * g.speed) * -CD : 0.0;
+    double jf1 = jet ? g.mr * (h.d1 * g.speed) * -CD : 0.0;
+    double jf2 = jet ? g.mr * (h.d2 * g.speed) * -CD : 0.0;
     /* added-mass force (src/dynamics.py:131-141) */
     double am0 = m * AMF0, am1 = m * AMF1, am2 = m * AMF2, amr = g.mr * AMRF;
     double amv0 = am0 * h.v0, amv1 = am1 * h.v1, amv2 = am2 * h.v2;
@@ -387,19 +391,15 @@ SD void tick(Hot& h, const Params& P) {
            ct2 = -(h.w0 * iw1 - h.w1 * iw0);
     /* drag torque (src/dynamics.py:119-128) */
     double wn = np_norm3(h.w0, h.w1, h.w2);
-    double dimx, dimy;
-    if (h.g32) { dimx = (double)cubef((float)h.W); dimy = (double)cubef((float)h.L); }
-    else { dimx = sm_cube(h.W); dimy = sm_cube(h.L); }
-    double rcd0 = 0.3 - g.nr * (0.3 - 0.1), rcd1 = 0.2 - g.nr * (0.2 - 0.5);
-    double ra0 = rcd0 * k * g.A0, ra1 = rcd1 * k * g.A1;
-    double dt0 = ra0 * wn * h.w0 * dimx + ra0 * h.w0 * h.W * DRAG_TORQUE_RATIO;
-    double dt1 = ra1 * wn * h.w1 * dimy + ra1 * h.w1 * h.W * DRAG_TORQUE_RATIO;
-    double dt2 = ra1 * wn * h.w2 * dimy + ra1 * h.w2 * h.W * DRAG_TORQUE_RATIO;
+    double dt0 = g.ra0 * wn * h.w0 * g.dimx + g.ra0 * h.w0 * h.W * DRAG_TORQUE_RATIO;
+    double dt1 = g.ra1 * wn * h.w1 * g.dimy + g.ra1 * h.w1 * h.W * DRAG_TORQUE_RATIO;
+    double dt2 = g.ra1 * wn * h.w2 * g.dimy + g.ra1 * h.w2 * h.W * DRAG_TORQUE_RATIO;
     /* jet torque r x F, r = (mid_x - L/2, 0, 0) (src/robot.py:931-935) */
-    double rx = P.mid_x + -h.L / 2.0;
-    double jt1 = -(rx * jf2), jt2 = rx * jf1;
+    double jt1 = -(g.rx * jf2), jt2 = g.rx * jf1;
     /* deformation torque -(dI/dt) w; prev_I <- I (src/robot.py:888-896) */
-    double ir0 = (I0 - h.pI0) / DT, ir1 = (I1 - h.pI1) / DT, ir2 = (I1 - h.pI2) / DT;
+    double ir0 = (I0 - h.pI0) / DT, ir1 = (I1 - h.pI1) / DT;
+    double ir2 = ir1;
+    if (h.pI2 != h.pI1) ir2 = (I1 - h.pI2) / DT;   /* prev_I[1,1] == prev_I[2,2] always */
     double dft0 = -(ir0 * h.w0), dft1 = -(ir1 * h.w1), dft2 = -(ir2 * h.w2);
     h.pI0 = I0; h.pI1 = I1; h.pI2 = I1;
     /* added-mass torque, I_rate term identically zero (src/dynamics.py:144-156) */
@@ -417,18 +417,19 @@ SD void tick(Hot& h, const Params& P) {
     /* ---------------- integrate (semi-implicit Euler) ---------------- */
     h.v0 = h.v0 + na0 * DT; h.v1 = h.v1 + na1 * DT; h.v2 = h.v2 + na2 * DT;
     h.w0 = h.w0 + nal0 * DT; h.w1 = h.w1 + nal1 * DT; h.w2 = h.w2 + nal2 * DT;
-    {   /* to_euler_angle_rate_jit (src/dynamics.py:20-31) */
-        double sp, cp, st, ctt;
-        sm_sincos(h.e0, &sp, &cp);
-        sm_sincos(h.e1, &st, &ctt);
-        double tt = st / ctt;
-        double r0 = sm_fma(cp * tt, h.w2, h.w0 + (sp * tt) * h.w1);
-        double r1 = sm_fma(-sp, h.w2, cp * h.w1);
-        double r2 = sm_fma(cp / ctt, h.w2, (sp / ctt) * h.w1);
+    {   /* to_euler_angle_rate_jit (src/dynamics.py:20-31) at the current angles */
+        double tt = h.st / h.cth;
+        double r0 = sm_fma(h.cp * tt, h.w2, h.w0 + (h.sp * tt) * h.w1);
+        double r1 = sm_fma(-h.sp, h.w2, h.cp * h.w1);
+        double r2 = sm_fma(h.cp / h.cth, h.w2, (h.sp / h.cth) * h.w1);
         h.e0 = h.e0 + r0 * DT; h.e1 = h.e1 + r1 * DT; h.e2 = h.e2 + r2 * DT;
     }
-    {   /* to_world_frame_jit (src/dynamics.py:34-58) */
-        Rot R = rot_zyx(h.e0, h.e1, h.e2);
+    {   /* to_world_frame_jit (src/dynamics.py:34-58) at the new angles */
+        double ss, cs;
+        sm_sincos(h.e0, &h.sp, &h.cp);
+        sm_sincos(h.e1, &h.st, &h.cth);
+        sm_sincos(h.e2, &ss, &cs);
+        Rot R = rot_sc(h.sp, h.cp, h.st, h.cth, ss, cs);
         double vw[3];
         rot_apply(R, h.v0, h.v1, h.v2, vw);
         h.p0 = h.p0 + vw[0] * DT; h.p1 = h.p1 + vw[1] * DT; h.p2 = h.p2 + vw[2] * DT;
@@ -441,16 +442,18 @@ SD void tick(Hot& h, const Params& P) {
     h.phase = h.ct <= h.mx ? REFILL : (h.ct <= h.b1 ? JET : (h.ct <= h.b2 ? COAST : REST));
     h.pV = h.V;
     h.pv32 = h.g32;
-    bool f32;
-    h.L = body_length(P, h.phase, h.ct, h.refill, h.mx, h.c, h.cr, h.rr, &f32);
-    h.W = body_width(P, h.phase, h.ct, h.refill, h.mx, h.c, h.cr, h.rr);
-    h.g32 = f32;
-    h.V = water_volume(P, h.L, h.W, f32);
-    double com = center_of_mass(P, h.L, h.W, water_mass(P, h.V, f32), f32);
+    bool f;
+    body_lw(P, h.phase, h.ct, h.refill, h.mx, h.c, h.cr, h.rr, &h.L, &h.W, &f);
+    h.g32 = f;
+    const Core c = core(h.L, h.W, f);
+    h.V = water_volume(P, c, f);
+    const double wm = water_mass(P, h.V, f);
+    double com = center_of_mass(P, c, wm, f);
     double comr = (com - h.com) / DT;
     h.coma = (comr - h.comr) / DT;
     h.com = com;
     h.comr = comr;
+    h.geo = make_geo(P, c, h.L, h.W, h.V, h.pV, h.g32, h.pv32, wm);
 }
 
 /* ------------------------------------------------ env-step prologue */
@@ -602,7 +605,8 @@ SD StepOut finish_step(const Hot& h, double* S, const Params& P, int64_t i, floa
     observation(h, R, S, P, i, obs);
     /* _check_obstacle_collision with get_current_length() */
     bool l32;
-    double Lc = body_length(P, h.phase, h.ct, h.refill, h.mx, h.c, h.cr, h.rr, &l32);
+    double Lc, Wc;
+    body_lw(P, h.phase, h.ct, h.refill, h.mx, h.c, h.cr, h.rr, &Lc, &Wc, &l32);
     double thr = l32 ? (double)((float)P.obstacle_radius + (float)Lc / 2.0f)
                      : P.obstacle_radius + Lc / 2;
     bool hit = false;
@@ -713,14 +717,18 @@ SD void reset_env(Hot& h, double* S, const Params& P, int64_t i, const float* tg
     h.q0 = h.q1 = h.q2 = 0.0; h.g0 = h.g1 = h.g2 = 0.0;
     SF(SALP_F_PPOS0) = 0.0; SF(SALP_F_PPOS1) = 0.0; SF(SALP_F_PPOS2) = 0.0;
     SF(SALP_F_PANG0) = 0.0; SF(SALP_F_PANG1) = 0.0; SF(SALP_F_PANG2) = 0.0;
-    h.com = center_of_mass(P, h.L, h.W, water_mass(P, h.V, h.g32), h.g32);
+    {
+        const Core old = core(h.L, h.W, h.g32);
+        h.com = center_of_mass(P, old, water_mass(P, h.V, h.g32), h.g32);
+    }
     h.comr = (h.com - h.com) / DT;
     h.coma = (h.comr - h.comr) / DT;
     h.L = P.L0; h.W = P.W0; h.g32 = false;
-    h.V = water_volume(P, h.L, h.W, false);
+    const Core c0 = core(h.L, h.W, false);
+    h.V = water_volume(P, c0, false);
     h.pV = h.V; h.pv32 = false;
-    Geo g = geometry(P, h.L, h.W, h.V, h.pV, false, false);
-    h.pI0 = g.I0; h.pI1 = g.I1; h.pI2 = g.I1;
+    refresh_derived(h, P);
+    h.pI0 = h.geo.I0; h.pI1 = h.geo.I1; h.pI2 = h.geo.I1;
     /* env trackers */
     const double d0 = h.p0 - (double)tgt[0], d1 = h.p1 - (double)tgt[1];
     const double dist = np_norm2(d0, d1);
@@ -750,16 +758,14 @@ SD void reset_env_philox(Hot& h, double* S, const Params& P, int64_t i, float* o
 /* Robot / Nozzle / SalpRobotEnv constructors (src/robot.py:20-47, 261-412) */
 SD void construct_env(double* S, const Params& P, int64_t i) {
     for (int f = 0; f < SALP_NUM_FIELDS; ++f) SF(f) = 0.0;
-    Hot h;
-    h.L = P.L0; h.W = P.W0; h.g32 = false; h.pv32 = false;
-    h.V = water_volume(P, h.L, h.W, false);
-    h.pV = h.V;
-    Geo g = geometry(P, h.L, h.W, h.V, h.pV, false, false);
-    SF(SALP_F_LENGTH) = h.L; SF(SALP_F_WIDTH) = h.W;
-    SF(SALP_F_VOLUME) = h.V; SF(SALP_F_PREV_VOLUME) = h.pV;
+    const Core c0 = core(P.L0, P.W0, false);
+    const double V = water_volume(P, c0, false);
+    const Geo g = make_geo(P, c0, P.L0, P.W0, V, V, false, false, water_mass(P, V, false));
+    SF(SALP_F_LENGTH) = P.L0; SF(SALP_F_WIDTH) = P.W0;
+    SF(SALP_F_VOLUME) = V; SF(SALP_F_PREV_VOLUME) = V;
     SF(SALP_F_PREV_I0) = g.I0; SF(SALP_F_PREV_I1) = g.I1; SF(SALP_F_PREV_I2) = g.I1;
     /* Robot.__init__ runs before set_environment: density 1000 */
-    SF(SALP_F_COM) = center_of_mass(P, h.L, h.W, 1000.0 * h.V, false);
+    SF(SALP_F_COM) = center_of_mass(P, c0, 1000.0 * V, false);
     SF(SALP_F_PHASE) = REST;
     /* make_env: nozzle.set_angles(init angles) */
     SF(SALP_F_ANGLE1) = P.init_angle1; SF(SALP_F_ANGLE2) = P.init_angle2;
