@@ -54,6 +54,7 @@ SIGNATURES = {
     "salp_get_state": (ctypes.c_int, [_H, _V, _V]),
     "salp_set_state": (ctypes.c_int, [_H, _V, _V]),
     "salp_state_ptr": (ctypes.c_int64, [_H]),
+    "salp_bench_ticks": (ctypes.c_int, [_H, ctypes.c_int32, _V]),
     "salp_math_selftest": (ctypes.c_int, [_V, _V, ctypes.c_int64, _V, _V]),
 }
 

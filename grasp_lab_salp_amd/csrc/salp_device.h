@@ -35,6 +35,7 @@
 #pragma clang fp contract(off)
 
 #define SD static __device__ __forceinline__
+#define SD_MEMBER __device__ __forceinline__
 
 namespace salp {
 
@@ -74,6 +75,17 @@ struct Params {
 
 /* ----------------------------------------------------------- helpers */
 SD double pymax(double a, double b) { return b > a ? b : a; }
+/* x / DT, correctly rounded, in 4 instructions instead of the ~11 of a general
+ * division: 1/0.01 rounds to exactly 100 with relative error 2^-55.4, so
+ * q0 = x*100 is within 1 ulp of x/DT and one FMA correction with the exact
+ * remainder yields the correctly rounded quotient (Markstein); div_fixup
+ * supplies the sign of zero and the inf/NaN cases.  Checked against x / 0.01
+ * on 4e8 random operands (tests/test_divdt.py keeps a sample). */
+SD double div_dt(double x) {
+    const double q0 = x * 100.0;
+    const double q = sm_fma(sm_fma(-DT, q0, x), 100.0, q0);
+    return __builtin_amdgcn_div_fixup(q, DT, x);
+}
 SD float sqf(float x) { return (float)((double)x * (double)x); }
 SD float cubef(float x) {
     double p = (double)x * (double)x;
@@ -192,14 +204,10 @@ struct Geo {
     double speed;                 /* jet speed (V - V_prev) / dt / A_nozzle */
     double rx;                    /* jet moment arm x */
 };
-SD Geo make_geo(const Params& P, const Core& c, double L, double W, double V, double pV, bool g32,
-                bool pv32, double wm) {
+SD Geo make_geo_shape(const Params& P, const Core& c, double L, double W, double wm, bool f) {
     Geo g;
-    const bool f = g32, b32 = g32 && pv32;
-    /* get_mass / get_mass_rate (src/robot.py:1061-1066, 651-654); wm = water mass */
-    double pwm = r32(sel(pv32, P.density) * pV, pv32);
+    /* get_mass (src/robot.py:1061-1066); wm = water mass */
     g.m = r32(r32(sel(f, P.dry_mass) + wm, f) + sel(f, P.nozzle_mass), f);
-    g.mr = r32(r32(wm - pwm, b32) / sel(b32, DT), b32);
     /* compute_cross_sectional_area_jit (src/geometry.py:67-75) */
     double pi = sel(f, PI);
     double A0 = r32(r32(pi * c.wh, f) * c.wh, f);
@@ -230,11 +238,54 @@ SD Geo make_geo(const Params& P, const Core& c, double L, double W, double V, do
     g.I0 = r32(p1 * sx, f) + r32(kw * sx, f);
     g.I1 = BUOY_MASS * c.lh2 + P.net_tube_mass * t8 + r32(p1 * sy, f) + r32(kw * sy, f) +
            P.nozzle_mass * n25;
-    /* compute_jet_velocity_jit speed (src/dynamics.py:87-94) */
-    g.speed = r32(r32(r32(V - pV, b32) / sel(b32, DT), b32) / sel(b32, P.nozzle_area), b32);
     /* compute_jet_moment_arm_jit (src/geometry.py:126-130) */
     g.rx = P.mid_x + -L / 2.0;
     return g;
+}
+/* get_mass_rate (src/robot.py:651-654) and compute_jet_velocity_jit speed
+ * (src/dynamics.py:87-94); float32 only when both volumes are float32. */
+SD void jet_rates(const Params& P, double V, double pV, double wm, bool g32, bool pv32, Geo& g) {
+    const bool b32 = g32 && pv32;
+    double pwm = r32(sel(pv32, P.density) * pV, pv32);
+    if (b32) {
+        g.mr = r32(r32(wm - pwm, true) / sel(true, DT), true);
+        g.speed = r32(r32(r32(V - pV, true) / sel(true, DT), true) / sel(true, P.nozzle_area), true);
+    } else {
+        g.mr = div_dt(wm - pwm);
+        g.speed = div_dt(V - pV) / P.nozzle_area;
+    }
+}
+SD Geo make_geo(const Params& P, const Core& c, double L, double W, double V, double pV, bool g32,
+                bool pv32, double wm) {
+    Geo g = make_geo_shape(P, c, L, W, wm, g32);
+    jet_rates(P, V, pV, wm, g32, pv32, g);
+    return g;
+}
+
+/* Float32-mode geometry of the current cycle.  While REFILL runs past
+ * refill_time the body is the float32 contracted shape (init_length -
+ * contraction, init_width + contraction) for every tick, so everything NumPy
+ * computes in float32 there is a per-cycle constant: computed once per cycle
+ * (begin_step / kernel start) into LDS, read back by the ticks whose lane is in
+ * that mode.  Ticks compute the float64 geometry only: no dtype selects. */
+enum { C32_V, C32_WM, C32_COM, C32_M, C32_I0, C32_I1, C32_KC0, C32_KC1, C32_RA0, C32_RA1, C32_DIMX,
+       C32_DIMY, C32_N };
+constexpr int LANES = 256;   /* workgroup size of every ticking kernel (LDS stride) */
+struct Cache32 {
+    double* p;               /* this lane's column of a [C32_N][LANES] LDS array */
+    SD_MEMBER double& operator[](int k) const { return p[k * LANES]; }
+};
+SD void fill_cache32(const Params& P, double contraction, Cache32 c32) {
+    const double L = (double)((float)P.L0 - (float)contraction);
+    const double W = (double)((float)P.W0 + (float)contraction);
+    const Core c = core(L, W, true);
+    const double V = water_volume(P, c, true);
+    const double wm = water_mass(P, V, true);
+    const Geo g = make_geo_shape(P, c, L, W, wm, true);
+    c32[C32_V] = V; c32[C32_WM] = wm; c32[C32_COM] = center_of_mass(P, c, wm, true);
+    c32[C32_M] = g.m; c32[C32_I0] = g.I0; c32[C32_I1] = g.I1;
+    c32[C32_KC0] = g.kc0; c32[C32_KC1] = g.kc1; c32[C32_RA0] = g.ra0; c32[C32_RA1] = g.ra1;
+    c32[C32_DIMX] = g.dimx; c32[C32_DIMY] = g.dimy;
 }
 
 /* compute_length_jit / compute_width_jit (src/geometry.py:39-64); in REFILL
@@ -276,7 +327,7 @@ SD void refresh_derived(Hot& h, const Params& P) {
     sm_sincos(h.e1, &h.st, &h.cth);
 }
 
-SD void load_hot(Hot& h, const double* S, const Params& P, int64_t i) {
+SD void load_hot(Hot& h, const double* S, const Params& P, int64_t i, bool derived = true) {
     h.v0 = SF(SALP_F_V0); h.v1 = SF(SALP_F_V1); h.v2 = SF(SALP_F_V2);
     h.w0 = SF(SALP_F_W0); h.w1 = SF(SALP_F_W1); h.w2 = SF(SALP_F_W2);
     h.a0 = SF(SALP_F_ACC0); h.a1 = SF(SALP_F_ACC1); h.a2 = SF(SALP_F_ACC2);
@@ -295,7 +346,7 @@ SD void load_hot(Hot& h, const double* S, const Params& P, int64_t i) {
     h.c = SF(SALP_F_CONTRACTION); h.cr = SF(SALP_F_CONTRACT_RATE); h.rr = SF(SALP_F_RELEASE_RATE);
     h.turn = SF(SALP_F_TURN_TIME);
     h.phase = (int)SF(SALP_F_PHASE);
-    refresh_derived(h, P);
+    if (derived) refresh_derived(h, P);
 }
 SD void store_hot(const Hot& h, double* S, const Params& P, int64_t i) {
     SF(SALP_F_V0) = h.v0; SF(SALP_F_V1) = h.v1; SF(SALP_F_V2) = h.v2;
@@ -348,7 +399,11 @@ SD void cycle_bounds(Hot& h) {
  * _newton_equations (:789-823), _euler_equations (:825-851),
  * _update_motion_states (:860-875); then cycle_time, update_state,
  * update_properties (:640-668). */
-SD void tick(Hot& h, const Params& P) {
+SD void tick(Hot& h, const Params& P, Cache32 c32) {
+    /* this cycle's float32-mode geometry, used at the end if the lane is in
+     * that mode (issued first so that the LDS latency hides under the tick) */
+    double k32[C32_N];
+    for (int k = 0; k < C32_N; ++k) k32[k] = c32[k];
     const Geo& g = h.geo;
     const double m = g.m;
     /* ---------------- Newton ---------------- */
@@ -397,9 +452,9 @@ SD void tick(Hot& h, const Params& P) {
     /* jet torque r x F, r = (mid_x - L/2, 0, 0) (src/robot.py:931-935) */
     double jt1 = -(g.rx * jf2), jt2 = g.rx * jf1;
     /* deformation torque -(dI/dt) w; prev_I <- I (src/robot.py:888-896) */
-    double ir0 = (I0 - h.pI0) / DT, ir1 = (I1 - h.pI1) / DT;
+    double ir0 = div_dt(I0 - h.pI0), ir1 = div_dt(I1 - h.pI1);
     double ir2 = ir1;
-    if (h.pI2 != h.pI1) ir2 = (I1 - h.pI2) / DT;   /* prev_I[1,1] == prev_I[2,2] always */
+    if (h.pI2 != h.pI1) ir2 = div_dt(I1 - h.pI2);   /* prev_I[1,1] == prev_I[2,2] always */
     double dft0 = -(ir0 * h.w0), dft1 = -(ir1 * h.w1), dft2 = -(ir2 * h.w2);
     h.pI0 = I0; h.pI1 = I1; h.pI2 = I1;
     /* added-mass torque, I_rate term identically zero (src/dynamics.py:144-156) */
@@ -445,21 +500,33 @@ SD void tick(Hot& h, const Params& P) {
     bool f;
     body_lw(P, h.phase, h.ct, h.refill, h.mx, h.c, h.cr, h.rr, &h.L, &h.W, &f);
     h.g32 = f;
-    const Core c = core(h.L, h.W, f);
-    h.V = water_volume(P, c, f);
-    const double wm = water_mass(P, h.V, f);
-    double com = center_of_mass(P, c, wm, f);
-    double comr = (com - h.com) / DT;
-    h.coma = (comr - h.comr) / DT;
+    /* float64 geometry (bitwise the f = false instance of the shared code),
+     * replaced by the cycle's float32 geometry where the lane is in that mode */
+    const Core c = core(h.L, h.W, false);
+    double V = water_volume(P, c, false);
+    double wm = water_mass(P, V, false);
+    double com = center_of_mass(P, c, wm, false);
+    Geo ng = make_geo_shape(P, c, h.L, h.W, wm, false);
+    if (f) {
+        V = k32[C32_V]; wm = k32[C32_WM]; com = k32[C32_COM];
+        ng.m = k32[C32_M]; ng.I0 = k32[C32_I0]; ng.I1 = k32[C32_I1];
+        ng.kc0 = k32[C32_KC0]; ng.kc1 = k32[C32_KC1]; ng.ra0 = k32[C32_RA0]; ng.ra1 = k32[C32_RA1];
+        ng.dimx = k32[C32_DIMX]; ng.dimy = k32[C32_DIMY];
+    }
+    h.V = V;
+    double comr = div_dt(com - h.com);
+    h.coma = div_dt(comr - h.comr);
     h.com = com;
     h.comr = comr;
-    h.geo = make_geo(P, c, h.L, h.W, h.V, h.pV, h.g32, h.pv32, wm);
+    jet_rates(P, V, h.pV, wm, f, h.pv32, ng);
+    h.geo = ng;
 }
 
 /* ------------------------------------------------ env-step prologue */
 /* SalpRobotEnv.step up to step_through_cycle's loop (src/salp_robot_env.py:
  * 196-210; src/robot.py:62-98 IK, :544-592 set_control, :740-748). */
-SD void begin_step(Hot& h, double* S, const Params& P, int64_t i, float a0, float a1, float a2) {
+SD void begin_step(Hot& h, double* S, const Params& P, int64_t i, float a0, float a1, float a2,
+                   Cache32 c32) {
     SF(SALP_F_ACT0) = a0; SF(SALP_F_ACT1) = a1; SF(SALP_F_ACT2) = a2;
     /* _rescale_action in float32 (src/salp_robot_env.py:166-174) */
     float r0 = a0 * 0.06f, r1 = a1 * 10.0f, r2 = a2 * (float)(PI / 2);
@@ -505,6 +572,7 @@ SD void begin_step(Hot& h, double* S, const Params& P, int64_t i, float a0, floa
     h.cr = h.refill > 0 ? h.c / h.refill : 0.0;
     h.rr = h.jet > 0 ? h.c / h.jet : 0.0;
     cycle_bounds(h);
+    fill_cache32(P, h.c, c32);
     /* step_through_cycle prologue (src/robot.py:742-748) */
     const double total = h.b2;
     double pq0 = SF(SALP_F_PPOS0), pq1 = SF(SALP_F_PPOS1), pq2 = SF(SALP_F_PPOS2);

@@ -25,8 +25,15 @@ constexpr int kBlock = 256;
 // 10 s < 1500 ticks.  The guard only bounds a lane fed a corrupted state.
 constexpr int kMaxTicksPerCycle = 1 << 16;
 
-__device__ __forceinline__ void run_cycle(Hot& h, const Params& P) {
-    for (int g = 0; h.ct < h.b2 && g < kMaxTicksPerCycle; ++g) salp::tick(h, P);
+static_assert(kBlock == salp::LANES, "LDS cache stride is the workgroup size");
+
+// This lane's column of the workgroup's per-cycle float32 geometry cache.
+#define LANE_CACHE32()                                              \
+    __shared__ double s_cache32[salp::C32_N * salp::LANES];         \
+    const salp::Cache32 c32{s_cache32 + threadIdx.x}
+
+__device__ __forceinline__ void run_cycle(Hot& h, const Params& P, salp::Cache32 c32) {
+    for (int g = 0; h.ct < h.b2 && g < kMaxTicksPerCycle; ++g) salp::tick(h, P, c32);
 }
 
 __global__ __launch_bounds__(kBlock) void k_construct(double* S, Params P) {
@@ -72,10 +79,11 @@ __global__ __launch_bounds__(kBlock) void k_step(double* S, Params P, const floa
                                                  double* info_out) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.n) return;
+    LANE_CACHE32();
     Hot h;
     salp::load_hot(h, S, P, i);
-    salp::begin_step(h, S, P, i, actions[3 * i], actions[3 * i + 1], actions[3 * i + 2]);
-    run_cycle(h, P);
+    salp::begin_step(h, S, P, i, actions[3 * i], actions[3 * i + 1], actions[3 * i + 2], c32);
+    run_cycle(h, P, c32);
     SF(SALP_F_STEP_COUNT) = SF(SALP_F_STEP_COUNT) + 1.0;
     float o[SALP_OBS_DIM_MAX];
     salp::StepOut r = salp::finish_step(h, S, P, i, o, info_out ? info_out + (size_t)SALP_INFO_DIM * i : nullptr);
@@ -95,6 +103,7 @@ __global__ __launch_bounds__(kBlock) void k_step_random(double* S, Params P, int
                                                         double* reward_sum) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.n) return;
+    LANE_CACHE32();
     Hot h;
     salp::load_hot(h, S, P, i);
     const uint64_t env_id = (uint64_t)(P.env_offset + i);
@@ -102,8 +111,8 @@ __global__ __launch_bounds__(kBlock) void k_step_random(double* S, Params P, int
     for (int32_t k = 0; k < n_steps; ++k) {
         float a[3];
         sp_action(P.seed, env_id, (uint64_t)SF(SALP_F_STEP_COUNT), a);
-        salp::begin_step(h, S, P, i, a[0], a[1], a[2]);
-        run_cycle(h, P);
+        salp::begin_step(h, S, P, i, a[0], a[1], a[2], c32);
+        run_cycle(h, P, c32);
         SF(SALP_F_STEP_COUNT) = SF(SALP_F_STEP_COUNT) + 1.0;
         float o[SALP_OBS_DIM_MAX];
         salp::StepOut r = salp::finish_step(h, S, P, i, o, nullptr);
@@ -126,7 +135,7 @@ __global__ __launch_bounds__(kBlock) void k_step_random(double* S, Params P, int
 __device__ __forceinline__ void rollout_boundary(Hot& h, double* S, const Params& P, int64_t i,
                                                  uint64_t env_id, bool& pending, bool& active,
                                                  int64_t& steps, int64_t max_steps,
-                                                 const SalpRolloutBuffers& B) {
+                                                 const SalpRolloutBuffers& B, salp::Cache32 c32) {
     // a few rounds so that zero-tick cycles chain without waiting a chunk
     for (int rep = 0; rep < 4; ++rep) {
         const bool fin = active && pending && !(h.ct < h.b2);
@@ -156,32 +165,92 @@ __device__ __forceinline__ void rollout_boundary(Hot& h, double* S, const Params
         if (beg) {
             float a[3];
             sp_action(P.seed, env_id, (uint64_t)SF(SALP_F_STEP_COUNT), a);
-            salp::begin_step(h, S, P, i, a[0], a[1], a[2]);
+            salp::begin_step(h, S, P, i, a[0], a[1], a[2], c32);
             pending = true;
         }
         if (!fin && !beg) break;
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_rollout(double* S, Params P, int64_t n_chunks,
-                                                    int32_t chunk, int64_t max_steps,
-                                                    SalpRolloutBuffers B) {
+// All launch arguments in one struct: the env-step epilogue re-reads them from
+// the kernarg segment (scalar loads) where it runs, so that nothing it needs
+// is held in SGPRs across the tick loop — which then compiles exactly like a
+// standalone tick loop (its polynomial constants stay resident in SGPRs).
+struct RolloutArgs {
+    double* S;
+    Params P;
+    int64_t n_chunks;
+    int32_t chunk;
+    int64_t max_steps;
+    SalpRolloutBuffers B;
+};
+static_assert(sizeof(RolloutArgs) % 8 == 0, "RolloutArgs is copied as 8-byte words");
+typedef const __attribute__((address_space(4))) uint64_t* KernargWords;
+__device__ __forceinline__ RolloutArgs fresh_args() {
+    KernargWords p = (KernargWords)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));   // opaque: the loads below stay where they are used
+    uint64_t w[sizeof(RolloutArgs) / 8];
+    for (size_t k = 0; k < sizeof(RolloutArgs) / 8; ++k) w[k] = p[k];
+    RolloutArgs a;
+    __builtin_memcpy(&a, w, sizeof a);
+    return a;
+}
+
+__global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
+    double* const S = A.S;
+    const Params& P = A.P;
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.n) return;
+    bool pending = SF(SALP_F_PENDING) != 0.0;
+    int64_t steps = A.B.steps_done ? A.B.steps_done[i] : 0;
+    bool active = !(A.max_steps > 0 && steps >= A.max_steps);
+    LANE_CACHE32();
     Hot h;
     salp::load_hot(h, S, P, i);
-    const uint64_t env_id = (uint64_t)(P.env_offset + i);
-    bool pending = SF(SALP_F_PENDING) != 0.0;
-    if (pending) salp::resume_cycle(h, S, P, i);
-    int64_t steps = B.steps_done ? B.steps_done[i] : 0;
-    bool active = !(max_steps > 0 && steps >= max_steps);
-    for (int64_t c = 0; c < n_chunks; ++c) {
-        rollout_boundary(h, S, P, i, env_id, pending, active, steps, max_steps, B);
-        for (int32_t k = 0; k < chunk; ++k)
-            if (active && h.ct < h.b2) salp::tick(h, P);
+    salp::resume_cycle(h, S, P, i);
+    salp::fill_cache32(P, h.c, c32);
+    if (!active) h.b2 = -INFINITY;
+    for (int64_t c = 0; c <= A.n_chunks; ++c) {
+        // Env-step boundary, taken by the whole wave when any lane needs it.
+        // The tick state goes through memory around it so that no register
+        // holds tick state while the (much larger) epilogue code runs.
+        const bool need = active && (!pending || !(h.ct < h.b2));
+        const bool last = c == A.n_chunks;
+        if (__any(need) || last) {
+            salp::store_hot(h, S, P, i);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            if (need) {
+                const RolloutArgs a = fresh_args();
+                const uint64_t env_id = (uint64_t)(a.P.env_offset + i);
+                Hot hb;
+                salp::load_hot(hb, a.S, a.P, i, false);
+                salp::resume_cycle(hb, a.S, a.P, i);
+                rollout_boundary(hb, a.S, a.P, i, env_id, pending, active, steps, a.max_steps, a.B, c32);
+                salp::store_hot(hb, a.S, a.P, i);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (last) break;
+            salp::load_hot(h, S, P, i);
+            salp::resume_cycle(h, S, P, i);
+            if (!active) h.b2 = -INFINITY;   // a finished lane ticks no more
+        }
+        for (int32_t k = 0; k < A.chunk; ++k)
+            if (h.ct < h.b2) salp::tick(h, P, c32);
     }
-    rollout_boundary(h, S, P, i, env_id, pending, active, steps, max_steps, B);
-    if (B.steps_done) B.steps_done[i] = steps;
+    if (A.B.steps_done) A.B.steps_done[i] = steps;
+}
+
+// Diagnostic: n_ticks physics ticks on every lane with no env-step boundaries
+// (cycles simply run on in REST), to time the tick body alone.
+__global__ __launch_bounds__(kBlock) void k_tick_bench(double* S, Params P, int32_t n_ticks) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    LANE_CACHE32();
+    Hot h;
+    salp::load_hot(h, S, P, i);
+    salp::resume_cycle(h, S, P, i);
+    salp::fill_cache32(P, h.c, c32);
+    for (int32_t k = 0; k < n_ticks; ++k) salp::tick(h, P, c32);
     salp::store_hot(h, S, P, i);
 }
 
@@ -396,8 +465,8 @@ int salp_rollout(SalpEnv* h, int64_t tick_budget, const SalpRolloutBuffers* buf,
     if (b.capacity < 0) return fail(h, SALP_EINVAL, "salp_rollout: capacity < 0");
     int32_t chunk = b.chunk > 0 ? b.chunk : 32;
     int64_t n_chunks = (tick_budget + chunk - 1) / chunk;
-    hipLaunchKernelGGL(k_rollout, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream,
-                       h->state, h->dp, n_chunks, chunk, b.max_steps, b);
+    RolloutArgs args{h->state, h->dp, n_chunks, chunk, b.max_steps, b};
+    hipLaunchKernelGGL(k_rollout, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream, args);
     return launched(h, "k_rollout");
 }
 
@@ -420,6 +489,13 @@ int salp_math_selftest(const double* x, const double* y, int64_t n, double* out,
     hipLaunchKernelGGL(k_math_selftest, dim3(blocks_for(n)), dim3(kBlock), 0, (hipStream_t)stream, x, y,
                        n, out);
     return check_hip(nullptr, hipGetLastError(), "k_math_selftest");
+}
+
+int salp_bench_ticks(SalpEnv* h, int32_t n_ticks, void* stream) {
+    if (!h || n_ticks < 0) return fail(h, SALP_EINVAL, "salp_bench_ticks: bad argument");
+    hipLaunchKernelGGL(k_tick_bench, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream,
+                       h->state, h->dp, n_ticks);
+    return launched(h, "k_tick_bench");
 }
 
 int64_t salp_state_ptr(SalpEnv* h) { return h ? (int64_t)(intptr_t)h->state : 0; }

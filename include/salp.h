@@ -144,6 +144,10 @@ int salp_num_fields(void);
 const char* salp_field_name(int field);
 int salp_get_state(SalpEnv* h, double* state_out, void* stream);
 int salp_set_state(SalpEnv* h, const double* state_in, void* stream);
+/* Diagnostic: n_ticks physics ticks on every env with no env-step boundaries
+ * (a cycle that ends simply continues in REST); times the tick body alone.
+ * Leaves the envs in a state no reference call sequence produces. */
+int salp_bench_ticks(SalpEnv* h, int32_t n_ticks, void* stream);
 /* Device address of the handle's state buffer (zero-copy views). */
 int64_t salp_state_ptr(SalpEnv* h);
 /* Device-side self-test of salp_math.h: out[i] = f(x[i]) for f in
