@@ -6,7 +6,7 @@ drift apart silently.
 """
 import ctypes
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_OBSTACLES = 4
 OBS_DIM_MAX = 6 + 2 * MAX_OBSTACLES
 
@@ -63,8 +63,8 @@ FIELDS = (
     + ["length", "width", "volume", "prev_volume", "com", "com_rate", "com_acc"]
     + _vec("prev_I") + ["geom32", "pvol32"]
     + ["cycle_time", "time", "refill_time", "jet_time", "coast_time", "contraction",
-       "contract_rate", "release_rate", "phase", "cycle"]
-    + ["angle1", "angle2", "yaw", "prev_yaw", "turn_time"]
+       "contract_rate", "release_rate", "phase", "cycle", "contr32"]
+    + ["angle1", "angle2", "prev_angle1", "prev_angle2", "yaw", "prev_yaw", "turn_time"]
     + ["target0", "target1"] + [f"obst{i}" for i in range(2 * MAX_OBSTACLES)]
     + ["n_obst", "prev_dist", "prev_a2"]
     + ["ep_len", "ep_return", "path_len", "last_px", "last_py", "sum_a0", "sum_a1", "sum_abs_a2",
@@ -89,3 +89,29 @@ REWARD_COMPONENT_KEYS = INFO_KEYS[:7]
 EPISODE_METRIC_KEYS = INFO_KEYS[7:23]
 
 PHASES = ("REFILL", "JET", "COAST", "REST")  # src/robot.py:252-257
+
+# Columns of a trace sample (enum SalpTraceCol in include/salp.h); names are
+# the reference's *_history attributes (src/robot.py:687-738) without the
+# suffix, vectors split per component.
+TRACE_COLUMNS = (
+    ["state"] + _vec("position_world") + _vec("velocity") + _vec("acceleration")
+    + _vec("euler_angle") + _vec("euler_angle_rate") + _vec("angular_velocity")
+    + _vec("angular_acceleration") + ["length", "width"] + _vec("area")
+    + ["volume", "mass", "mass_rate", "nozzle_yaw"] + _vec("inertia_tensor")
+    + _vec("trans_drag_coefficient") + _vec("rot_drag_coefficient")
+    + ["center_of_mass", "center_of_mass_rate", "center_of_mass_acc_rate"]
+    + _vec("position_front_world")
+    + _vec("jet_velocity") + _vec("jet_force") + _vec("jet_torque") + _vec("drag_force")
+    + _vec("drag_torque") + _vec("coriolis_force") + _vec("coriolis_torque")
+    + _vec("added_mass_force") + _vec("added_mass_torque") + _vec("deform_torque")
+    + _vec("acceleration_force")
+)
+TRACE_DIM = len(TRACE_COLUMNS)
+TRACE = {k: i for i, k in enumerate(TRACE_COLUMNS)}
+TRACE_FIRST_FORCE = TRACE["jet_velocity0"]
+# history name -> (first column, width) ; width 1 = scalar history
+TRACE_HISTORIES = {}
+for _i, _k in enumerate(TRACE_COLUMNS):
+    _base = _k[:-1] if _k[-1] in "012" and _k[:-1] + "1" in TRACE else _k
+    if _base not in TRACE_HISTORIES:
+        TRACE_HISTORIES[_base] = (_i, 3 if _base != _k else 1)

@@ -7,7 +7,7 @@ no CPU fallback: if the library or a GPU is missing, :func:`lib` raises.
 import ctypes
 import os
 
-from ._abi import ABI_VERSION, FIELDS, NUM_FIELDS, SalpParams
+from ._abi import ABI_VERSION, FIELDS, NUM_FIELDS, TRACE_DIM, SalpParams
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libsalp.so")
@@ -33,6 +33,14 @@ class SalpRolloutBuffers(ctypes.Structure):
     ]
 
 
+class SalpTraceBuffer(ctypes.Structure):
+    _fields_ = [
+        ("max_samples", ctypes.c_int64),
+        ("rows", ctypes.c_void_p),
+        ("n_samples", ctypes.c_void_p),
+    ]
+
+
 # name -> (restype, argtypes); exactly the functions declared in include/salp.h
 _V, _H = ctypes.c_void_p, ctypes.c_void_p
 SIGNATURES = {
@@ -49,8 +57,15 @@ SIGNATURES = {
     "salp_step": (ctypes.c_int, [_H, _V, _V, _V, _V, _V, ctypes.c_int, _V, _V, _V]),
     "salp_rollout": (ctypes.c_int, [_H, ctypes.c_int64, ctypes.POINTER(SalpRolloutBuffers), _V]),
     "salp_step_random": (ctypes.c_int, [_H, ctypes.c_int32, _V, _V]),
+    "salp_robot_reset": (ctypes.c_int, [_H, _V, _V]),
+    "salp_nozzle_set_angles": (ctypes.c_int, [_H, _V, _V]),
+    "salp_nozzle_solve": (ctypes.c_int, [_H, _V, ctypes.c_int, _V]),
+    "salp_robot_set_control": (ctypes.c_int, [_H, _V, ctypes.c_int, _V]),
+    "salp_robot_step_through_cycle": (ctypes.c_int, [_H, _V]),
+    "salp_set_trace": (ctypes.c_int, [_H, ctypes.POINTER(SalpTraceBuffer)]),
     "salp_num_fields": (ctypes.c_int, []),
     "salp_field_name": (ctypes.c_char_p, [ctypes.c_int]),
+    "salp_trace_dim": (ctypes.c_int, []),
     "salp_get_state": (ctypes.c_int, [_H, _V, _V]),
     "salp_set_state": (ctypes.c_int, [_H, _V, _V]),
     "salp_state_ptr": (ctypes.c_int64, [_H]),
@@ -76,6 +91,8 @@ def load(path=LIB_PATH):
         raise SalpError("libsalp ABI version mismatch")
     if L.salp_num_fields() != NUM_FIELDS:
         raise SalpError("libsalp state layout does not match grasp_lab_salp_amd._abi")
+    if L.salp_trace_dim() != TRACE_DIM:
+        raise SalpError("libsalp trace layout does not match grasp_lab_salp_amd._abi")
     for i, name in enumerate(FIELDS):
         if L.salp_field_name(i).decode() != name:
             raise SalpError(f"field {i}: library says {L.salp_field_name(i)!r}, _abi says {name!r}")

@@ -12,7 +12,7 @@ import torch
 
 from . import _lib
 from ._abi import (EPISODE_METRIC_KEYS, FIELD, FIELDS, INFO, INFO_DIM, INFO_KEYS, MAX_OBSTACLES,
-                   NUM_FIELDS, REWARD_COMPONENT_KEYS, SalpParams, default_params)
+                   NUM_FIELDS, REWARD_COMPONENT_KEYS, TRACE_DIM, SalpParams, default_params)
 
 __all__ = ["BatchedSalpEnv", "StepResult"]
 
@@ -67,7 +67,8 @@ class BatchedSalpEnv:
         self._h = h
         self.obs_dim = L.salp_obs_dim(h)
         self.num_obstacles = self.params.num_obstacles
-        self._info = torch.zeros((self.n_envs, INFO_DIM), dtype=torch.float64, device=self.device)
+        self._trace = None
+        self.version = 0   # bumped by every call that changes the device state
 
     # ------------------------------------------------------------ plumbing
     @property
@@ -78,6 +79,11 @@ class BatchedSalpEnv:
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
     def _check(self, rc):
+        return _lib.check(rc, self._h)
+
+    def _run(self, rc):
+        """check + mark the state as changed (host-side caches key on version)."""
+        self.version += 1
         return _lib.check(rc, self._h)
 
     def close(self):
@@ -108,7 +114,7 @@ class BatchedSalpEnv:
         uses the process-global np.random, src/salp_robot_env.py:484-487)."""
         obs = torch.zeros((self.n_envs, self.obs_dim), dtype=torch.float32, device=self.device)
         m = self._mask(mask)
-        self._check(_lib.load().salp_reset(self._h, _ptr(m), _ptr(obs), self._stream()))
+        self._run(_lib.load().salp_reset(self._h, _ptr(m), _ptr(obs), self._stream()))
         return obs
 
     def reset_to(self, targets, obstacles, n_obstacles=None, mask=None):
@@ -122,7 +128,7 @@ class BatchedSalpEnv:
         k = torch.as_tensor(n_obstacles, device=self.device).reshape(self.n_envs).to(torch.int32).contiguous()
         obs = torch.zeros((self.n_envs, self.obs_dim), dtype=torch.float32, device=self.device)
         m = self._mask(mask)
-        self._check(_lib.load().salp_reset_to(self._h, _ptr(m), _ptr(t), _ptr(o.contiguous()), _ptr(k),
+        self._run(_lib.load().salp_reset_to(self._h, _ptr(m), _ptr(t), _ptr(o.contiguous()), _ptr(k),
                                               _ptr(obs), self._stream()))
         return obs
 
@@ -139,7 +145,7 @@ class BatchedSalpEnv:
         tobs = (torch.empty((self.n_envs, self.obs_dim), dtype=torch.float32, device=self.device)
                 if want_terminal_obs else None)
         info = torch.empty((self.n_envs, INFO_DIM), dtype=torch.float64, device=self.device)
-        self._check(_lib.load().salp_step(self._h, _ptr(a), _ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc),
+        self._run(_lib.load().salp_step(self._h, _ptr(a), _ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc),
                                           int(bool(auto_reset)), _ptr(tobs), _ptr(info), self._stream()))
         return StepResult(obs, rew, term.bool(), trunc.bool(), tobs, info)
 
@@ -147,7 +153,7 @@ class BatchedSalpEnv:
         """n_steps synthetic random-action env-steps per env (lock-step, auto-reset).
         Returns the per-env reward sum (fp64)."""
         rs = torch.empty(self.n_envs, dtype=torch.float64, device=self.device)
-        self._check(_lib.load().salp_step_random(self._h, int(n_steps), _ptr(rs), self._stream()))
+        self._run(_lib.load().salp_step_random(self._h, int(n_steps), _ptr(rs), self._stream()))
         return rs
 
     def rollout(self, tick_budget, buffers=None, steps_done=None, max_steps=0, chunk=32):
@@ -175,8 +181,65 @@ class BatchedSalpEnv:
             B.steps_done = steps_done.data_ptr()
         B.max_steps = int(max_steps)
         B.chunk = int(chunk)
-        self._check(_lib.load().salp_rollout(self._h, int(tick_budget), ctypes.byref(B), self._stream()))
+        self._run(_lib.load().salp_rollout(self._h, int(tick_budget), ctypes.byref(B), self._stream()))
         return steps_done
+
+    # ------------------------------------------- Robot / Nozzle level
+    # The reference's bare-robot call sequence (src/compare_trajectories.py:
+    # 142-150): nozzle.set_yaw_angle + solve_angles, set_control,
+    # step_through_cycle.  Arguments are per-env tensors; *_f32 says the
+    # reference would hold an np.float32 there instead of a Python float.
+    def _f64(self, x, shape):
+        return torch.as_tensor(x, dtype=torch.float64, device=self.device).reshape(shape).contiguous()
+
+    def robot_reset(self, mask=None):
+        """Robot.reset() (src/robot.py:452-501) of every (or every masked) env."""
+        m = self._mask(mask)
+        self._run(_lib.load().salp_robot_reset(self._h, _ptr(m), self._stream()))
+
+    def nozzle_set_angles(self, angles):
+        """Nozzle.set_angles(angle1, angle2) (src/robot.py:50-60); angles [n, 2]."""
+        a = self._f64(angles, (self.n_envs, 2))
+        self._run(_lib.load().salp_nozzle_set_angles(self._h, _ptr(a), self._stream()))
+
+    def nozzle_solve(self, yaw, yaw_f32=False):
+        """Nozzle.set_yaw_angle(yaw) + Nozzle.solve_angles() (src/robot.py:62-98)."""
+        y = self._f64(yaw, (self.n_envs,))
+        self._run(_lib.load().salp_nozzle_solve(self._h, _ptr(y), int(bool(yaw_f32)), self._stream()))
+
+    def robot_set_control(self, control, contraction_f32=False):
+        """Robot.set_control(contraction, coast_time, [angle1, angle2])
+        (src/robot.py:544-592); control [n, 4]."""
+        c = self._f64(control, (self.n_envs, 4))
+        self._run(_lib.load().salp_robot_set_control(self._h, _ptr(c), int(bool(contraction_f32)),
+                                                       self._stream()))
+
+    def robot_step_through_cycle(self):
+        """Robot.step_through_cycle() (src/robot.py:740-777) of every env."""
+        self._run(_lib.load().salp_robot_step_through_cycle(self._h, self._stream()))
+
+    # --------------------------------------------------------- recording
+    def enable_trace(self, max_samples):
+        """Robot.enable_history_recording: from now on step() and
+        robot_step_through_cycle() record per-tick samples of the last cycle
+        (columns _abi.TRACE_COLUMNS) into device buffers; see :meth:`trace`."""
+        rows = torch.full((int(max_samples), TRACE_DIM, self.n_envs), float("nan"), dtype=torch.float64,
+                          device=self.device)
+        ns = torch.zeros(self.n_envs, dtype=torch.int64, device=self.device)
+        B = _lib.SalpTraceBuffer(int(max_samples), rows.data_ptr(), ns.data_ptr())
+        self._check(_lib.load().salp_set_trace(self._h, ctypes.byref(B)))
+        self._trace = (rows, ns)
+
+    def disable_trace(self):
+        self._check(_lib.load().salp_set_trace(self._h, None))
+        self._trace = None
+
+    def trace(self):
+        """(rows [max_samples, TRACE_DIM, n] fp64, n_samples [n] int64) of the
+        last recorded cycle; rows past n_samples are stale."""
+        if self._trace is None:
+            raise _lib.SalpError("recording is not enabled (enable_trace)")
+        return self._trace
 
     # ------------------------------------------------------------ state
     def get_state(self):
@@ -188,7 +251,7 @@ class BatchedSalpEnv:
     def set_state(self, state):
         s = torch.as_tensor(state, dtype=torch.float64, device=self.device).reshape(NUM_FIELDS, self.n_envs)
         s = s.contiguous()
-        self._check(_lib.load().salp_set_state(self._h, _ptr(s), self._stream()))
+        self._run(_lib.load().salp_set_state(self._h, _ptr(s), self._stream()))
         torch.cuda.current_stream(self.device).synchronize()
 
     def field(self, name):

@@ -204,24 +204,37 @@ struct Geo {
     double speed;                 /* jet speed (V - V_prev) / dt / A_nozzle */
     double rx;                    /* jet moment arm x */
 };
+/* compute_cross_sectional_area_jit (src/geometry.py:67-75): A0 = area[0],
+ * A1 = area[1] = area[2]; compute_drag_coefficient_jit (src/geometry.py:
+ * 104-123): the clipped interpolation ratio nr of the coefficient ranges. */
+struct Shape { double A0, A1, nr; };
+SD Shape shape_of(const Params& P, const Core& c, double L, double W, bool f) {
+    Shape s;
+    double pi = sel(f, PI);
+    s.A0 = r32(r32(pi * c.wh, f) * c.wh, f);
+    s.A1 = r32(r32(pi * c.lh, f) * c.wh, f);
+    double aspect = r32(L / W, f);
+    double nr = r32(r32(aspect - sel(f, P.end_aspect), f) / sel(f, P.aspect_den), f);
+    nr = nr < 0.0 ? 0.0 : nr;
+    s.nr = nr > 1.0 ? 1.0 : nr;
+    return s;
+}
+/* trans / rot drag-coefficient ranges (src/robot.py:415-434) at ratio nr */
+SD double tcd_x(double nr) { return 2.5 - nr * (2.5 - 1.5); }
+SD double tcd_y(double nr) { return 1.5 - nr * (1.5 - 2.5); }
+SD double rcd_x(double nr) { return 0.3 - nr * (0.3 - 0.1); }
+SD double rcd_y(double nr) { return 0.2 - nr * (0.2 - 0.5); }
 SD Geo make_geo_shape(const Params& P, const Core& c, double L, double W, double wm, bool f) {
     Geo g;
     /* get_mass (src/robot.py:1061-1066); wm = water mass */
     g.m = r32(r32(sel(f, P.dry_mass) + wm, f) + sel(f, P.nozzle_mass), f);
-    /* compute_cross_sectional_area_jit (src/geometry.py:67-75) */
-    double pi = sel(f, PI);
-    double A0 = r32(r32(pi * c.wh, f) * c.wh, f);
-    double A1 = r32(r32(pi * c.lh, f) * c.wh, f);
-    /* compute_drag_coefficient_jit (src/geometry.py:104-123) */
-    double aspect = r32(L / W, f);
-    double nr = r32(r32(aspect - sel(f, P.end_aspect), f) / sel(f, P.aspect_den), f);
-    nr = nr < 0.0 ? 0.0 : nr;
-    nr = nr > 1.0 ? 1.0 : nr;
+    const Shape sh = shape_of(P, c, L, W, f);
+    const double A0 = sh.A0, A1 = sh.A1, nr = sh.nr;
     /* compute_drag_force_jit / compute_drag_torque_jit coefficients
      * (src/dynamics.py:110-128; ranges src/robot.py:415-434) */
     const double k = -0.5 * P.density;
-    double tcd0 = 2.5 - nr * (2.5 - 1.5), tcd1 = 1.5 - nr * (1.5 - 2.5);
-    double rcd0 = 0.3 - nr * (0.3 - 0.1), rcd1 = 0.2 - nr * (0.2 - 0.5);
+    double tcd0 = tcd_x(nr), tcd1 = tcd_y(nr);
+    double rcd0 = rcd_x(nr), rcd1 = rcd_y(nr);
     g.kc0 = r32(A0 * k, f) * tcd0;
     g.kc1 = r32(A1 * k, f) * tcd1;
     g.ra0 = rcd0 * k * A0;
@@ -288,17 +301,20 @@ SD void fill_cache32(const Params& P, double contraction, Cache32 c32) {
     c32[C32_DIMX] = g.dimx; c32[C32_DIMY] = g.dimy;
 }
 
-/* compute_length_jit / compute_width_jit (src/geometry.py:39-64); in REFILL
- * past refill_time both are np.float32 (`init_length - contraction`), in JET
- * that float32 difference is the first operand of a float64 sum. */
+/* compute_length_jit / compute_width_jit (src/geometry.py:39-64).  With an
+ * np.float32 contraction (c32, the env path) `init_length - contraction` is
+ * np.float32: in REFILL past refill_time the body is float32, in JET that
+ * float32 difference is the first operand of a float64 sum.  With a Python
+ * float contraction everything is float64. */
 SD void body_lw(const Params& P, int phase, double ct, double refill, double mx, double c,
-                double cr, double rr, double* L, double* W, bool* f32) {
+                double cr, double rr, bool c32, double* L, double* W, bool* f32) {
     const bool fill = phase == REFILL, jet = phase == JET, early = ct < refill;
-    const double Lc = (double)((float)P.L0 - (float)c), Wc = (double)((float)P.W0 + (float)c);
+    const double Lc = c32 ? (double)((float)P.L0 - (float)c) : P.L0 - c;
+    const double Wc = c32 ? (double)((float)P.W0 + (float)c) : P.W0 + c;
     const double x = (ct - mx) * rr;
     *L = fill ? (early ? P.L0 - ct * cr : Lc) : (jet ? Lc + x : P.L0);
     *W = fill ? (early ? P.W0 + ct * cr : Wc) : (jet ? Wc - x : P.W0);
-    *f32 = fill && !early;
+    *f32 = fill && !early && c32;
 }
 
 /* ---------------------------------------------------- per-lane state */
@@ -313,7 +329,7 @@ struct Hot {
     double sp, cp, st, cth;                                    /* sin/cos of roll, pitch */
     Geo geo;                                                   /* geometry of (L, W, V, pV) */
     int phase;
-    bool g32, pv32;
+    bool g32, pv32, c32;
 };
 
 #define SF(f) S[(size_t)(f) * (size_t)P.n + (size_t)i]
@@ -346,6 +362,7 @@ SD void load_hot(Hot& h, const double* S, const Params& P, int64_t i, bool deriv
     h.c = SF(SALP_F_CONTRACTION); h.cr = SF(SALP_F_CONTRACT_RATE); h.rr = SF(SALP_F_RELEASE_RATE);
     h.turn = SF(SALP_F_TURN_TIME);
     h.phase = (int)SF(SALP_F_PHASE);
+    h.c32 = SF(SALP_F_CONTR32) != 0.0;
     if (derived) refresh_derived(h, P);
 }
 SD void store_hot(const Hot& h, double* S, const Params& P, int64_t i) {
@@ -367,6 +384,7 @@ SD void store_hot(const Hot& h, double* S, const Params& P, int64_t i) {
     SF(SALP_F_CONTRACTION) = h.c; SF(SALP_F_CONTRACT_RATE) = h.cr; SF(SALP_F_RELEASE_RATE) = h.rr;
     SF(SALP_F_TURN_TIME) = h.turn;
     SF(SALP_F_PHASE) = (double)h.phase;
+    SF(SALP_F_CONTR32) = h.c32 ? 1.0 : 0.0;
 }
 
 /* Nozzle.get_nozzle_direction (src/robot.py:138-150): R_br @ R_mb @ R_nm @
@@ -399,7 +417,11 @@ SD void cycle_bounds(Hot& h) {
  * _newton_equations (:789-823), _euler_equations (:825-851),
  * _update_motion_states (:860-875); then cycle_time, update_state,
  * update_properties (:640-668). */
-SD void tick(Hot& h, const Params& P, Cache32 c32) {
+/* Recording (REC): rec points at this env's column of a trace sample,
+ * rec[col * rs] (include/salp.h SalpTraceBuffer); the force columns are
+ * written here, the state columns by record_state after the tick. */
+template <bool REC = false>
+SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_t rs = 0) {
     /* this cycle's float32-mode geometry, used at the end if the lane is in
      * that mode (issued first so that the LDS latency hides under the tick) */
     double k32[C32_N];
@@ -467,6 +489,23 @@ SD void tick(Hot& h, const Params& P, Cache32 c32) {
     double nal0 = (((dt0 + ct0) + dft0) + amt0) / I0;
     double nal1 = ((((jt1 + dt1) + ct1) + dft1) + amt1) / I1;
     double nal2 = ((((jt2 + dt2) + ct2) + dft2) + amt2) / I1;
+    if (REC) {
+        const double z = 0.0;
+        auto put = [&](int col, double x) { rec[(int64_t)col * rs] = x; };
+        put(SALP_T_JETV0, jet ? h.d0 * g.speed : 0.0);
+        put(SALP_T_JETV1, jet ? h.d1 * g.speed : 0.0);
+        put(SALP_T_JETV2, jet ? h.d2 * g.speed : 0.0);
+        put(SALP_T_JETF0, jf0); put(SALP_T_JETF1, jf1); put(SALP_T_JETF2, jf2);
+        put(SALP_T_JETT0, z * jf2 - z * jf1); put(SALP_T_JETT1, jt1); put(SALP_T_JETT2, jt2);
+        put(SALP_T_DRAGF0, df0); put(SALP_T_DRAGF1, df1); put(SALP_T_DRAGF2, df2);
+        put(SALP_T_DRAGT0, dt0); put(SALP_T_DRAGT1, dt1); put(SALP_T_DRAGT2, dt2);
+        put(SALP_T_CORF0, cf0); put(SALP_T_CORF1, cf1); put(SALP_T_CORF2, cf2);
+        put(SALP_T_CORT0, ct0); put(SALP_T_CORT1, ct1); put(SALP_T_CORT2, ct2);
+        put(SALP_T_AMF0, af0); put(SALP_T_AMF1, af1); put(SALP_T_AMF2, af2);
+        put(SALP_T_AMT0, amt0); put(SALP_T_AMT1, amt1); put(SALP_T_AMT2, amt2);
+        put(SALP_T_DEFT0, dft0); put(SALP_T_DEFT1, dft1); put(SALP_T_DEFT2, dft2);
+        put(SALP_T_ACCF0, ff0); put(SALP_T_ACCF1, ff1); put(SALP_T_ACCF2, ff2);
+    }
     h.a0 = na0; h.a1 = na1; h.a2 = na2;
     h.al0 = nal0; h.al1 = nal1; h.al2 = nal2;
     /* ---------------- integrate (semi-implicit Euler) ---------------- */
@@ -478,6 +517,11 @@ SD void tick(Hot& h, const Params& P, Cache32 c32) {
         double r1 = sm_fma(-h.sp, h.w2, h.cp * h.w1);
         double r2 = sm_fma(h.cp / h.cth, h.w2, (h.sp / h.cth) * h.w1);
         h.e0 = h.e0 + r0 * DT; h.e1 = h.e1 + r1 * DT; h.e2 = h.e2 + r2 * DT;
+        if (REC) {
+            rec[(int64_t)SALP_T_ETAR0 * rs] = r0;
+            rec[(int64_t)SALP_T_ETAR1 * rs] = r1;
+            rec[(int64_t)SALP_T_ETAR2 * rs] = r2;
+        }
     }
     {   /* to_world_frame_jit (src/dynamics.py:34-58) at the new angles */
         double ss, cs;
@@ -498,7 +542,7 @@ SD void tick(Hot& h, const Params& P, Cache32 c32) {
     h.pV = h.V;
     h.pv32 = h.g32;
     bool f;
-    body_lw(P, h.phase, h.ct, h.refill, h.mx, h.c, h.cr, h.rr, &h.L, &h.W, &f);
+    body_lw(P, h.phase, h.ct, h.refill, h.mx, h.c, h.cr, h.rr, h.c32, &h.L, &h.W, &f);
     h.g32 = f;
     /* float64 geometry (bitwise the f = false instance of the shared code),
      * replaced by the cycle's float32 geometry where the lane is in that mode */
@@ -522,21 +566,25 @@ SD void tick(Hot& h, const Params& P, Cache32 c32) {
     h.geo = ng;
 }
 
-/* ------------------------------------------------ env-step prologue */
-/* SalpRobotEnv.step up to step_through_cycle's loop (src/salp_robot_env.py:
- * 196-210; src/robot.py:62-98 IK, :544-592 set_control, :740-748). */
-SD void begin_step(Hot& h, double* S, const Params& P, int64_t i, float a0, float a1, float a2,
-                   Cache32 c32) {
-    SF(SALP_F_ACT0) = a0; SF(SALP_F_ACT1) = a1; SF(SALP_F_ACT2) = a2;
-    /* _rescale_action in float32 (src/salp_robot_env.py:166-174) */
-    float r0 = a0 * 0.06f, r1 = a1 * 10.0f, r2 = a2 * (float)(PI / 2);
-    /* Nozzle.set_yaw_angle + solve_angles */
+/* ------------------------------------------- Nozzle / Robot control */
+/* Nozzle.set_yaw_angle + Nozzle.solve_angles (src/robot.py:62-98).  yaw32:
+ * the yaw is an np.float32 (env path, src/salp_robot_env.py:207), so np.cos /
+ * np.sin run in float32; otherwise in float64. */
+SD void nozzle_solve(double* S, const Params& P, int64_t i, double yaw, bool yaw32) {
     SF(SALP_F_PREV_YAW) = SF(SALP_F_YAW);
-    SF(SALP_F_YAW) = (double)r2;
-    double pa1 = SF(SALP_F_ANGLE1), pa2 = SF(SALP_F_ANGLE2);
-    float sy, cy;
-    sm_np_sincosf(r2, &sy, &cy);
-    double t1 = -(double)sy, t2 = (double)cy;        /* R_br^T @ -[cos, sin, 0] */
+    SF(SALP_F_YAW) = yaw;
+    SF(SALP_F_PREV_ANGLE1) = SF(SALP_F_ANGLE1);
+    SF(SALP_F_PREV_ANGLE2) = SF(SALP_F_ANGLE2);
+    double sy, cy;
+    if (yaw32) {
+        float s, c;
+        sm_np_sincosf((float)yaw, &s, &c);
+        sy = s; cy = c;
+    } else {
+        sm_sincos(yaw, &sy, &cy);
+    }
+    /* R_br.T @ -[cos, sin, 0] = [-0, -sin, cos] */
+    double t1 = -sy, t2 = cy;
     double val2 = 2.0 * t2 - 1.0;
     if (val2 < -1.0) val2 = -1.0;
     if (val2 > 1.0) val2 = 1.0;
@@ -557,23 +605,44 @@ SD void begin_step(Hot& h, double* S, const Params& P, int64_t i, float a0, floa
     }
     if (an1 <= -PI) an1 += 2 * PI;
     else if (an1 > PI) an1 -= 2 * PI;
-    /* set_control -> Nozzle.set_angles (src/robot.py:50-60, 173-185) */
-    SF(SALP_F_ANGLE1) = an1; SF(SALP_F_ANGLE2) = an2;
-    h.turn = fabs(an1 - pa1) / P.angle_speed + fabs(an2 - pa2) / P.angle_speed;
-    nozzle_direction(an1, an2, &h.d0);
-    /* set_control (src/robot.py:577-592, geometry.py:14-26) */
+    SF(SALP_F_ANGLE1) = an1;
+    SF(SALP_F_ANGLE2) = an2;
+}
+
+/* Nozzle.set_angles -> _nozzle_turn_time (src/robot.py:50-60, 173-185) */
+SD double nozzle_set_angles(double* S, const Params& P, int64_t i, double a1, double a2) {
+    SF(SALP_F_ANGLE1) = a1;
+    SF(SALP_F_ANGLE2) = a2;
+    const double turn = fabs(a1 - SF(SALP_F_PREV_ANGLE1)) / P.angle_speed +
+                        fabs(a2 - SF(SALP_F_PREV_ANGLE2)) / P.angle_speed;
+    SF(SALP_F_TURN_TIME) = turn;
+    return turn;
+}
+
+/* Robot.set_control (src/robot.py:544-592, geometry.py:14-26); c32: the
+ * contraction is an np.float32 (contraction**2 is then float32). */
+SD void set_control(Hot& h, double* S, const Params& P, int64_t i, double contraction, double coast,
+                    double a1, double a2, bool c32) {
+    SF(SALP_F_AVGV0) = 0.0; SF(SALP_F_AVGV1) = 0.0; SF(SALP_F_AVGV2) = 0.0;
+    SF(SALP_F_AVGW0) = 0.0; SF(SALP_F_AVGW1) = 0.0; SF(SALP_F_AVGW2) = 0.0;
+    h.c = contraction;
+    h.coast = coast;
+    h.c32 = c32;
+    h.turn = nozzle_set_angles(S, P, i, a1, a2);
+    nozzle_direction(a1, a2, &h.d0);
     SF(SALP_F_CYCLE) = SF(SALP_F_CYCLE) + 1.0;
-    h.c = (double)r0;
-    h.coast = (double)r1;
     h.ct = 0.0;
-    double sq = (double)sqf(r0);
+    const double sq = c32 ? (double)sqf((float)h.c) : h.c * h.c;
     h.refill = REFILL_C0 * sq + REFILL_C1 * h.c + REFILL_C2;
     h.jet = PROPUL_C0 * sq + PROPUL_C1 * h.c + PROPUL_C2;
     h.cr = h.refill > 0 ? h.c / h.refill : 0.0;
     h.rr = h.jet > 0 ? h.c / h.jet : 0.0;
     cycle_bounds(h);
-    fill_cache32(P, h.c, c32);
-    /* step_through_cycle prologue (src/robot.py:742-748) */
+}
+
+/* Robot.step_through_cycle prologue (src/robot.py:740-748): the previous
+ * cycle's displacement over this cycle's total time. */
+SD void cycle_prologue(const Hot& h, double* S, const Params& P, int64_t i) {
     const double total = h.b2;
     double pq0 = SF(SALP_F_PPOS0), pq1 = SF(SALP_F_PPOS1), pq2 = SF(SALP_F_PPOS2);
     double pg0 = SF(SALP_F_PANG0), pg1 = SF(SALP_F_PANG1), pg2 = SF(SALP_F_PANG2);
@@ -584,6 +653,59 @@ SD void begin_step(Hot& h, double* S, const Params& P, int64_t i, float a0, floa
     SF(SALP_F_PPOS0) = h.q0; SF(SALP_F_PPOS1) = h.q1; SF(SALP_F_PPOS2) = h.q2;
     SF(SALP_F_PANG0) = h.g0; SF(SALP_F_PANG1) = h.g1; SF(SALP_F_PANG2) = h.g2;
     SF(SALP_F_PENDING) = 1.0;
+}
+
+/* ------------------------------------------------ env-step prologue */
+/* SalpRobotEnv.step up to step_through_cycle's loop (src/salp_robot_env.py:
+ * 196-210): float32 action rescale, IK, set_control, cycle prologue. */
+SD void begin_step(Hot& h, double* S, const Params& P, int64_t i, float a0, float a1, float a2,
+                   Cache32 c32) {
+    SF(SALP_F_ACT0) = a0; SF(SALP_F_ACT1) = a1; SF(SALP_F_ACT2) = a2;
+    /* _rescale_action in float32 (src/salp_robot_env.py:166-174) */
+    float r0 = a0 * 0.06f, r1 = a1 * 10.0f, r2 = a2 * (float)(PI / 2);
+    nozzle_solve(S, P, i, (double)r2, true);
+    set_control(h, S, P, i, (double)r0, (double)r1, SF(SALP_F_ANGLE1), SF(SALP_F_ANGLE2), true);
+    fill_cache32(P, h.c, c32);
+    cycle_prologue(h, S, P, i);
+}
+
+/* Trace sample: the state columns (src/robot.py:687-716) of the current
+ * state.  first: sample 0 of a cycle, whose force / rate columns are NaN. */
+SD void record_state(const Hot& h, const Params& P, const double* S, int64_t i, double* rec,
+                     int64_t rs, bool first) {
+    auto put = [&](int col, double x) { rec[(int64_t)col * rs] = x; };
+    put(SALP_T_STATE, (double)h.phase);
+    put(SALP_T_PW0, h.p0); put(SALP_T_PW1, h.p1); put(SALP_T_PW2, h.p2);
+    put(SALP_T_V0, h.v0); put(SALP_T_V1, h.v1); put(SALP_T_V2, h.v2);
+    put(SALP_T_ACC0, h.a0); put(SALP_T_ACC1, h.a1); put(SALP_T_ACC2, h.a2);
+    put(SALP_T_ETA0, h.e0); put(SALP_T_ETA1, h.e1); put(SALP_T_ETA2, h.e2);
+    put(SALP_T_W0, h.w0); put(SALP_T_W1, h.w1); put(SALP_T_W2, h.w2);
+    put(SALP_T_ALPHA0, h.al0); put(SALP_T_ALPHA1, h.al1); put(SALP_T_ALPHA2, h.al2);
+    put(SALP_T_LENGTH, h.L); put(SALP_T_WIDTH, h.W);
+    const Core c = core(h.L, h.W, h.g32);
+    const Shape sh = shape_of(P, c, h.L, h.W, h.g32);
+    put(SALP_T_AREA0, sh.A0); put(SALP_T_AREA1, sh.A1); put(SALP_T_AREA2, sh.A1);
+    put(SALP_T_VOLUME, h.V);
+    put(SALP_T_MASS, h.geo.m);
+    put(SALP_T_MASS_RATE, h.geo.mr);
+    put(SALP_T_I0, h.geo.I0); put(SALP_T_I1, h.geo.I1); put(SALP_T_I2, h.geo.I1);
+    put(SALP_T_TCD0, tcd_x(sh.nr)); put(SALP_T_TCD1, tcd_y(sh.nr)); put(SALP_T_TCD2, tcd_y(sh.nr));
+    put(SALP_T_RCD0, rcd_x(sh.nr)); put(SALP_T_RCD1, rcd_y(sh.nr)); put(SALP_T_RCD2, rcd_y(sh.nr));
+    put(SALP_T_COM, h.com); put(SALP_T_COM_RATE, h.comr); put(SALP_T_COM_ACC, h.coma);
+    /* get_front_position_world_frame (src/robot.py:924-928) */
+    const Rot R = rot_zyx(h.e0, h.e1, h.e2);
+    double fw[3];
+    rot_apply(R, h.L / 2, 0.0, 0.0, fw);
+    put(SALP_T_FRONT_W0, fw[0]); put(SALP_T_FRONT_W1, fw[1]); put(SALP_T_FRONT_W2, fw[2]);
+    if (first) {
+        for (int k = SALP_T_FIRST_FORCE; k < SALP_TRACE_DIM; ++k) put(k, NAN);
+        put(SALP_T_ETAR0, NAN); put(SALP_T_ETAR1, NAN); put(SALP_T_ETAR2, NAN);
+        put(SALP_T_NOZZLE_YAW, NAN);
+    } else {
+        /* Nozzle.step(cycle_time) (src/robot.py:101-108) */
+        const double yaw = SF(SALP_F_YAW), pyaw = SF(SALP_F_PREV_YAW);
+        put(SALP_T_NOZZLE_YAW, h.ct < h.turn ? pyaw + (h.ct / h.turn) * (yaw - pyaw) : yaw);
+    }
 }
 
 /* Resume an in-flight cycle: derived per-cycle values from stored ones. */
@@ -674,7 +796,7 @@ SD StepOut finish_step(const Hot& h, double* S, const Params& P, int64_t i, floa
     /* _check_obstacle_collision with get_current_length() */
     bool l32;
     double Lc, Wc;
-    body_lw(P, h.phase, h.ct, h.refill, h.mx, h.c, h.cr, h.rr, &Lc, &Wc, &l32);
+    body_lw(P, h.phase, h.ct, h.refill, h.mx, h.c, h.cr, h.rr, h.c32, &Lc, &Wc, &l32);
     double thr = l32 ? (double)((float)P.obstacle_radius + (float)Lc / 2.0f)
                      : P.obstacle_radius + Lc / 2;
     bool hit = false;
@@ -766,17 +888,11 @@ SD int draw_reset(const Params& P, uint64_t env_id, uint64_t episode, float* tgt
     return n;
 }
 
-/* SalpRobotEnv.reset with the target / obstacles given (src/salp_robot_env.py:
- * 114-155) -> Robot.reset (src/robot.py:452-501). */
-SD void reset_env(Hot& h, double* S, const Params& P, int64_t i, const float* tgt,
-                  const float* obst, int nob, float* obs) {
-    SF(SALP_F_TARGET0) = tgt[0]; SF(SALP_F_TARGET1) = tgt[1];
-    for (int k = 0; k < SALP_MAX_OBSTACLES; ++k) {
-        SF(SALP_F_OBST0 + 2 * k) = k < nob ? (double)obst[2 * k] : 0.0;
-        SF(SALP_F_OBST0 + 2 * k + 1) = k < nob ? (double)obst[2 * k + 1] : 0.0;
-    }
-    SF(SALP_F_N_OBST) = nob;
-    /* Robot.reset: kinematics zeroed; COM from the PREVIOUS geometry */
+/* Robot.reset (src/robot.py:452-501): kinematics zeroed, body back to the
+ * initial shape; the center of mass is taken from the PREVIOUS geometry
+ * (get_center_of_mass runs before length/width are reset); nozzle angles are
+ * not reset. */
+SD void robot_reset(Hot& h, double* S, const Params& P, int64_t i) {
     h.time = 0.0; h.ct = 0.0; h.phase = REST;
     SF(SALP_F_CYCLE) = 0.0;
     h.v0 = h.v1 = h.v2 = 0.0; h.w0 = h.w1 = h.w2 = 0.0;
@@ -797,6 +913,20 @@ SD void reset_env(Hot& h, double* S, const Params& P, int64_t i, const float* tg
     h.pV = h.V; h.pv32 = false;
     refresh_derived(h, P);
     h.pI0 = h.geo.I0; h.pI1 = h.geo.I1; h.pI2 = h.geo.I1;
+    SF(SALP_F_PENDING) = 0.0;
+}
+
+/* SalpRobotEnv.reset with the target / obstacles given (src/salp_robot_env.py:
+ * 114-155) -> Robot.reset. */
+SD void reset_env(Hot& h, double* S, const Params& P, int64_t i, const float* tgt,
+                  const float* obst, int nob, float* obs) {
+    SF(SALP_F_TARGET0) = tgt[0]; SF(SALP_F_TARGET1) = tgt[1];
+    for (int k = 0; k < SALP_MAX_OBSTACLES; ++k) {
+        SF(SALP_F_OBST0 + 2 * k) = k < nob ? (double)obst[2 * k] : 0.0;
+        SF(SALP_F_OBST0 + 2 * k + 1) = k < nob ? (double)obst[2 * k + 1] : 0.0;
+    }
+    SF(SALP_F_N_OBST) = nob;
+    robot_reset(h, S, P, i);
     /* env trackers */
     const double d0 = h.p0 - (double)tgt[0], d1 = h.p1 - (double)tgt[1];
     const double dist = np_norm2(d0, d1);

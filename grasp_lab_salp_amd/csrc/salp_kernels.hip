@@ -36,6 +36,26 @@ __device__ __forceinline__ void run_cycle(Hot& h, const Params& P, salp::Cache32
     for (int g = 0; h.ct < h.b2 && g < kMaxTicksPerCycle; ++g) salp::tick(h, P, c32);
 }
 
+// The loop of Robot.step_through_cycle with record=True (src/robot.py:
+// 750-765): sample 0 before the first tick, one sample per tick after it.
+__device__ void run_cycle_recorded(Hot& h, const double* S, const Params& P, salp::Cache32 c32,
+                                   const SalpTraceBuffer& T, int64_t i) {
+    const int64_t n = P.n;
+    if (T.max_samples > 0) salp::record_state(h, P, S, i, T.rows + i, n, true);
+    int64_t t = 0;
+    for (int g = 0; h.ct < h.b2 && g < kMaxTicksPerCycle; ++g) {
+        ++t;
+        if (t < T.max_samples) {
+            double* rec = T.rows + (size_t)t * SALP_TRACE_DIM * (size_t)n + (size_t)i;
+            salp::tick<true>(h, P, c32, rec, n);
+            salp::record_state(h, P, S, i, rec, n, false);
+        } else {
+            salp::tick(h, P, c32);
+        }
+    }
+    T.n_samples[i] = t + 1;
+}
+
 __global__ __launch_bounds__(kBlock) void k_construct(double* S, Params P) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.n) return;
@@ -72,18 +92,20 @@ __global__ __launch_bounds__(kBlock) void k_reset_to(double* S, Params P, const 
 }
 
 // SalpRobotEnv.step for every env (one breathing cycle each).
+template <bool REC>
 __global__ __launch_bounds__(kBlock) void k_step(double* S, Params P, const float* actions,
                                                  float* obs_out, double* reward_out,
                                                  uint8_t* term_out, uint8_t* trunc_out,
                                                  int auto_reset, float* term_obs_out,
-                                                 double* info_out) {
+                                                 double* info_out, SalpTraceBuffer T) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.n) return;
     LANE_CACHE32();
     Hot h;
     salp::load_hot(h, S, P, i);
     salp::begin_step(h, S, P, i, actions[3 * i], actions[3 * i + 1], actions[3 * i + 2], c32);
-    run_cycle(h, P, c32);
+    if (REC) run_cycle_recorded(h, S, P, c32, T, i);
+    else run_cycle(h, P, c32);
     SF(SALP_F_STEP_COUNT) = SF(SALP_F_STEP_COUNT) + 1.0;
     float o[SALP_OBS_DIM_MAX];
     salp::StepOut r = salp::finish_step(h, S, P, i, o, info_out ? info_out + (size_t)SALP_INFO_DIM * i : nullptr);
@@ -240,6 +262,55 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
     if (A.B.steps_done) A.B.steps_done[i] = steps;
 }
 
+// ------------------------------------------------ Robot / Nozzle level
+__global__ __launch_bounds__(kBlock) void k_robot_reset(double* S, Params P, const uint8_t* mask) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n || (mask && !mask[i])) return;
+    Hot h;
+    salp::load_hot(h, S, P, i, false);
+    salp::robot_reset(h, S, P, i);
+    salp::store_hot(h, S, P, i);
+}
+
+__global__ __launch_bounds__(kBlock) void k_nozzle_set_angles(double* S, Params P, const double* ang) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    (void)salp::nozzle_set_angles(S, P, i, ang[2 * i], ang[2 * i + 1]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_nozzle_solve(double* S, Params P, const double* yaw,
+                                                         int yaw32) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    salp::nozzle_solve(S, P, i, yaw[i], yaw32 != 0);
+}
+
+__global__ __launch_bounds__(kBlock) void k_robot_set_control(double* S, Params P, const double* ctl,
+                                                              int c32) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    Hot h;
+    salp::load_hot(h, S, P, i, false);
+    salp::set_control(h, S, P, i, ctl[4 * i], ctl[4 * i + 1], ctl[4 * i + 2], ctl[4 * i + 3], c32 != 0);
+    salp::store_hot(h, S, P, i);
+}
+
+template <bool REC>
+__global__ __launch_bounds__(kBlock) void k_robot_cycle(double* S, Params P, SalpTraceBuffer T) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    LANE_CACHE32();
+    Hot h;
+    salp::load_hot(h, S, P, i);
+    salp::resume_cycle(h, S, P, i);
+    salp::fill_cache32(P, h.c, c32);
+    salp::cycle_prologue(h, S, P, i);
+    if (REC) run_cycle_recorded(h, S, P, c32, T, i);
+    else run_cycle(h, P, c32);
+    SF(SALP_F_PENDING) = 0.0;
+    salp::store_hot(h, S, P, i);
+}
+
 // Diagnostic: n_ticks physics ticks on every lane with no env-step boundaries
 // (cycles simply run on in REST), to time the tick body alone.
 __global__ __launch_bounds__(kBlock) void k_tick_bench(double* S, Params P, int32_t n_ticks) {
@@ -278,8 +349,8 @@ const char* const kFieldNames[SALP_NUM_FIELDS] = {
     "length", "width", "volume", "prev_volume", "com", "com_rate", "com_acc",
     "prev_I0", "prev_I1", "prev_I2", "geom32", "pvol32",
     "cycle_time", "time", "refill_time", "jet_time", "coast_time", "contraction",
-    "contract_rate", "release_rate", "phase", "cycle",
-    "angle1", "angle2", "yaw", "prev_yaw", "turn_time",
+    "contract_rate", "release_rate", "phase", "cycle", "contr32",
+    "angle1", "angle2", "prev_angle1", "prev_angle2", "yaw", "prev_yaw", "turn_time",
     "target0", "target1", "obst0", "obst1", "obst2", "obst3", "obst4", "obst5", "obst6", "obst7",
     "n_obst", "prev_dist", "prev_a2",
     "ep_len", "ep_return", "path_len", "last_px", "last_py", "sum_a0", "sum_a1", "sum_abs_a2",
@@ -296,6 +367,7 @@ struct SalpEnv {
     SalpParams params{};
     Params dp{};
     double* state = nullptr;
+    SalpTraceBuffer trace{};   // max_samples 0: not recording
     std::string err;
 };
 
@@ -417,6 +489,7 @@ const char* salp_last_error(const SalpEnv* h) {
 int64_t salp_num_envs(const SalpEnv* h) { return h ? h->n : -1; }
 int salp_obs_dim(const SalpEnv* h) { return h ? h->dp.obs_dim : -1; }
 int salp_num_fields(void) { return SALP_NUM_FIELDS; }
+int salp_trace_dim(void) { return SALP_TRACE_DIM; }
 const char* salp_field_name(int f) {
     return (f >= 0 && f < SALP_NUM_FIELDS) ? kFieldNames[f] : nullptr;
 }
@@ -443,9 +516,14 @@ int salp_step(SalpEnv* h, const float* actions, float* obs_out, double* reward_o
               float* terminal_obs_out, double* info_out, void* stream) {
     if (!h) return fail(nullptr, SALP_EINVAL, "salp_step: null handle");
     if (!actions) return fail(h, SALP_EINVAL, "salp_step: actions is required");
-    hipLaunchKernelGGL(k_step, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream,
-                       h->state, h->dp, actions, obs_out, reward_out, terminated_out, truncated_out,
-                       auto_reset, terminal_obs_out, info_out);
+    if (h->trace.max_samples > 0)
+        hipLaunchKernelGGL(k_step<true>, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream,
+                           h->state, h->dp, actions, obs_out, reward_out, terminated_out, truncated_out,
+                           auto_reset, terminal_obs_out, info_out, h->trace);
+    else
+        hipLaunchKernelGGL(k_step<false>, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream,
+                           h->state, h->dp, actions, obs_out, reward_out, terminated_out, truncated_out,
+                           auto_reset, terminal_obs_out, info_out, h->trace);
     return launched(h, "k_step");
 }
 
@@ -468,6 +546,60 @@ int salp_rollout(SalpEnv* h, int64_t tick_budget, const SalpRolloutBuffers* buf,
     RolloutArgs args{h->state, h->dp, n_chunks, chunk, b.max_steps, b};
     hipLaunchKernelGGL(k_rollout, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream, args);
     return launched(h, "k_rollout");
+}
+
+int salp_robot_reset(SalpEnv* h, const uint8_t* mask, void* stream) {
+    if (!h) return fail(nullptr, SALP_EINVAL, "salp_robot_reset: null handle");
+    hipLaunchKernelGGL(k_robot_reset, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream,
+                       h->state, h->dp, mask);
+    return launched(h, "k_robot_reset");
+}
+
+int salp_nozzle_set_angles(SalpEnv* h, const double* angles, void* stream) {
+    if (!h) return fail(nullptr, SALP_EINVAL, "salp_nozzle_set_angles: null handle");
+    if (!angles) return fail(h, SALP_EINVAL, "salp_nozzle_set_angles: angles is required");
+    hipLaunchKernelGGL(k_nozzle_set_angles, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream,
+                       h->state, h->dp, angles);
+    return launched(h, "k_nozzle_set_angles");
+}
+
+int salp_nozzle_solve(SalpEnv* h, const double* yaw, int yaw_is_f32, void* stream) {
+    if (!h) return fail(nullptr, SALP_EINVAL, "salp_nozzle_solve: null handle");
+    if (!yaw) return fail(h, SALP_EINVAL, "salp_nozzle_solve: yaw is required");
+    hipLaunchKernelGGL(k_nozzle_solve, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream,
+                       h->state, h->dp, yaw, yaw_is_f32);
+    return launched(h, "k_nozzle_solve");
+}
+
+int salp_robot_set_control(SalpEnv* h, const double* control, int contraction_is_f32, void* stream) {
+    if (!h) return fail(nullptr, SALP_EINVAL, "salp_robot_set_control: null handle");
+    if (!control) return fail(h, SALP_EINVAL, "salp_robot_set_control: control is required");
+    hipLaunchKernelGGL(k_robot_set_control, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream,
+                       h->state, h->dp, control, contraction_is_f32);
+    return launched(h, "k_robot_set_control");
+}
+
+int salp_robot_step_through_cycle(SalpEnv* h, void* stream) {
+    if (!h) return fail(nullptr, SALP_EINVAL, "salp_robot_step_through_cycle: null handle");
+    if (h->trace.max_samples > 0)
+        hipLaunchKernelGGL(k_robot_cycle<true>, dim3(blocks_for(h->n)), dim3(kBlock), 0,
+                           (hipStream_t)stream, h->state, h->dp, h->trace);
+    else
+        hipLaunchKernelGGL(k_robot_cycle<false>, dim3(blocks_for(h->n)), dim3(kBlock), 0,
+                           (hipStream_t)stream, h->state, h->dp, h->trace);
+    return launched(h, "k_robot_cycle");
+}
+
+int salp_set_trace(SalpEnv* h, const SalpTraceBuffer* buf) {
+    if (!h) return fail(nullptr, SALP_EINVAL, "salp_set_trace: null handle");
+    if (!buf || buf->max_samples <= 0) {
+        h->trace = SalpTraceBuffer{};
+        return SALP_OK;
+    }
+    if (!buf->rows || !buf->n_samples)
+        return fail(h, SALP_EINVAL, "salp_set_trace: rows and n_samples are required");
+    h->trace = *buf;
+    return SALP_OK;
 }
 
 int salp_get_state(SalpEnv* h, double* state_out, void* stream) {

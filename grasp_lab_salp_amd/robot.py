@@ -1,0 +1,316 @@
+"""Drop-in ``Nozzle`` / ``Robot`` (reference: src/robot.py:7-1086).
+
+Same constructor signatures, method names and attribute names as the
+reference, so ``make_env`` of src/train_robot.py:11-21 and
+src/train_robot_recurrent_ppo.py:29-38 runs unchanged.  The physics does not
+run here: a Robot is bound to one env of a :class:`BatchedSalpEnv` (its own
+1-env simulator for a standalone robot, or the env of the
+:class:`~grasp_lab_salp_amd.salp_robot_env.SalpRobotEnv` it is handed to),
+every method is a call into libsalp.so (HIP, gfx950), and every state
+attribute is read from the device state.  There is no CPU fallback: without a
+ROCm GPU the first simulating call raises.
+
+Before binding (between the constructor and the first simulating call) the
+objects only hold constructor arguments and the nozzle angles of
+``Nozzle.set_angles`` / ``Robot.set_environment``, exactly what ``make_env``
+sets up.
+"""
+from enum import Enum
+
+import numpy as np
+
+from ._abi import FIELD, TRACE, TRACE_HISTORIES, default_params
+
+__all__ = ["Nozzle", "Robot"]
+
+_ANGLE_SPEED = 31 * np.pi / 30   # src/robot.py:44
+
+
+def _f32_or_f64(x):
+    """Whether NumPy would hold x as an np.float32 (NEP 50 dtype of a control)."""
+    return isinstance(x, np.float32) or (isinstance(x, np.ndarray) and x.dtype == np.float32)
+
+
+class Nozzle:
+    """src/robot.py:7-208.  Geometry is fixed at construction; angles live on
+    the device once the owning Robot is bound."""
+
+    def __init__(self, length1: float = 0.0, length2: float = 0.0, length3: float = 0.0,
+                 area: float = 0.0, mass: float = 0.0):
+        self.length1, self.length2, self.length3 = length1, length2, length3
+        self.area, self.mass = area, mass
+        self.gamma = np.pi / 4
+        self.angle_speed = _ANGLE_SPEED
+        self._robot = None
+        # unbound values (src/robot.py:30-44)
+        self._local = dict(angle1=0.0, angle2=0.0, prev_angle1=0.0, prev_angle2=0.0, yaw=0.0,
+                           prev_yaw=0.0, turn_time=0.0)
+        self._pending_yaw = None
+
+    # ---- state (device once bound)
+    def _get(self, name):
+        if self._robot is not None and self._robot._bound:
+            if name == "yaw" and self._pending_yaw is not None:
+                return self._pending_yaw[0]
+            return float(self._robot._row()[FIELD[name]])
+        return self._local[name]
+
+    angle1 = property(lambda self: self._get("angle1"))
+    angle2 = property(lambda self: self._get("angle2"))
+    prev_angle1 = property(lambda self: self._get("prev_angle1"))
+    prev_angle2 = property(lambda self: self._get("prev_angle2"))
+    yaw = property(lambda self: self._get("yaw"))
+    prev_yaw = property(lambda self: self._get("prev_yaw"))
+    turn_time = property(lambda self: self._get("turn_time"))
+
+    # ---- control (src/robot.py:50-98)
+    def set_angles(self, angle1: float, angle2: float):
+        """Set the nozzle angles; turn time from the angles of the last solve."""
+        r = self._robot
+        if r is not None and r._bound:
+            r._env.nozzle_set_angles(np.array([[angle1, angle2]] * r._env.n_envs, np.float64))
+            return
+        L = self._local
+        L["angle1"], L["angle2"] = float(angle1), float(angle2)
+        L["turn_time"] = (abs(L["angle1"] - L["prev_angle1"]) / self.angle_speed
+                          + abs(L["angle2"] - L["prev_angle2"]) / self.angle_speed)
+
+    def set_yaw_angle(self, yaw_angle: float):
+        """Target yaw; applied (with prev_yaw <- yaw) by :meth:`solve_angles`."""
+        self._pending_yaw = (yaw_angle, _f32_or_f64(yaw_angle))
+
+    def solve_angles(self):
+        """Inverse kinematics for the pending yaw (src/robot.py:71-98), on the device."""
+        r = self._robot
+        if r is None:
+            raise RuntimeError("Nozzle.solve_angles needs the nozzle to belong to a Robot")
+        r._ensure_bound()
+        if self._pending_yaw is None:
+            yaw, f32 = self._get("yaw"), False
+        else:
+            yaw, f32 = self._pending_yaw
+        r._env.nozzle_solve(np.full(r._env.n_envs, float(yaw)), yaw_f32=f32)
+        self._pending_yaw = None
+
+    def step(self, time: float):
+        """Cosmetic yaw interpolation (src/robot.py:101-108); the recorded
+        ``nozzle_yaw_history`` carries it, nothing else reads it."""
+
+
+class Robot:
+    """src/robot.py:245-1086 — see the module docstring."""
+
+    class Phase(Enum):
+        REFILL = 0
+        JET = 1
+        COAST = 2
+        REST = 3
+
+    phase = [Phase.REFILL, Phase.JET, Phase.COAST, Phase.REST]
+
+    def __init__(self, dry_mass: float, init_length: float, init_width: float,
+                 max_contraction: float, nozzle: Nozzle):
+        self.dry_mass = dry_mass
+        self.init_length = init_length
+        self.init_width = init_width
+        self.max_contraction = max_contraction
+        self.nozzle = nozzle
+        nozzle._robot = self
+        self.buoy_mass, self.skin_mass, self.tube_mass = 0.195, 0.145, 0.414
+        self.density = 1000
+        self.dt = 0.01
+        self.tube_volume = np.pi * (0.058 / 2) ** 2 * 0.15
+        self.dynamics_randomization = False
+        self.disturbances = False
+        self.record = False
+        self._env = None
+        self._index = 0
+        self._owner = None     # the SalpRobotEnv this robot belongs to, if any
+        self._cache = (None, None)
+        self._clear_history()
+
+    # ------------------------------------------------------------ config
+    def set_environment(self, density: float):
+        if self._bound:
+            raise RuntimeError("set_environment must be called before the robot is simulated")
+        self.density = density
+
+    def enable_dynamic_randomization(self):
+        self.dynamics_randomization = True
+
+    def enable_disturbances(self):
+        self.disturbances = True
+
+    def enable_history_recording(self):
+        self.record = True
+        if self._bound and self._owner is None:
+            self._env.enable_trace(self._trace_capacity())
+
+    def disable_history_recording(self):
+        self.record = False
+        if self._bound and self._owner is None:
+            self._env.disable_trace()
+
+    def salp_params(self, **env_kwargs):
+        """The SalpParams the device needs for this robot (+ env arguments)."""
+        if self.dynamics_randomization or self.disturbances:
+            raise NotImplementedError(
+                "domain randomisation / OU disturbances (src/robot.py:210-242, 594-628) are not "
+                "implemented on the device yet; they are off in every reference script")
+        n = self.nozzle
+        return default_params(
+            nozzle_length1=float(n.length1), nozzle_length2=float(n.length2),
+            nozzle_length3=float(n.length3), nozzle_area=float(n.area), nozzle_mass=float(n.mass),
+            dry_mass=float(self.dry_mass), init_length=float(self.init_length),
+            init_width=float(self.init_width), max_contraction=float(self.max_contraction),
+            density=float(self.density), init_angle1=float(n._local["angle1"]),
+            init_angle2=float(n._local["angle2"]), **env_kwargs)
+
+    # ----------------------------------------------------------- binding
+    @property
+    def _bound(self):
+        return self._env is not None
+
+    def _bind(self, env, index=0, owner=None):
+        self._env, self._index, self._owner = env, int(index), owner
+        self._cache = (None, None)
+
+    def _ensure_bound(self):
+        if self._env is None:
+            from .batched_env import BatchedSalpEnv
+            self._bind(BatchedSalpEnv(1, params=self.salp_params()))
+            if self.record:
+                self._env.enable_trace(self._trace_capacity())
+
+    @staticmethod
+    def _trace_capacity():
+        # longest cycle: max(refill 3.3 s, turn 3.9 s) + jet + coast 10 s < 1500 ticks
+        return 2048
+
+    def _row(self):
+        """This robot's column of the device state (cached per state version)."""
+        ver, row = self._cache
+        if ver != self._env.version or row is None:
+            row = self._env.get_state()[:, self._index].cpu().numpy()
+            self._cache = (self._env.version, row)
+        return row
+
+    def _f(self, name):
+        return float(self._row()[FIELD[name]])
+
+    def _v(self, prefix):
+        r = self._row()
+        return np.array([r[FIELD[f"{prefix}{k}"]] for k in range(3)])
+
+    # ----------------------------------------------------- reference API
+    def reset(self):
+        """Robot.reset() (src/robot.py:452-501)."""
+        self._ensure_bound()
+        m = None
+        if self._env.n_envs > 1:
+            m = np.zeros(self._env.n_envs, np.uint8)
+            m[self._index] = 1
+        self._env.robot_reset(mask=m)
+        self._clear_history()
+
+    def set_control(self, contraction: float, coast_time: float, nozzle_angles):
+        """Robot.set_control (src/robot.py:544-592)."""
+        self._ensure_bound()
+        if self._env.n_envs != 1:
+            raise RuntimeError("per-robot control of a batched env: use BatchedSalpEnv.robot_set_control")
+        a = np.asarray(nozzle_angles, np.float64).reshape(2)
+        self._env.robot_set_control([[float(contraction), float(coast_time), a[0], a[1]]],
+                                    contraction_f32=_f32_or_f64(contraction))
+        self._clear_history()
+
+    def step_through_cycle(self):
+        """Robot.step_through_cycle (src/robot.py:740-777); with recording on,
+        fills the *_history attributes of the cycle."""
+        self._ensure_bound()
+        if self._env.n_envs != 1:
+            raise RuntimeError("per-robot stepping of a batched env: use BatchedSalpEnv")
+        self._env.robot_step_through_cycle()
+        if self.record:
+            self._load_history()
+
+    # ---------------------------------------------------------- histories
+    def _clear_history(self):
+        for h in TRACE_HISTORIES:
+            setattr(self, f"{h}_history", [])
+        self.asymmetry_torque_history = []
+        self.position_front_history = []
+
+    def _load_history(self):
+        """*_history arrays of the last recorded cycle (src/robot.py:766-777)."""
+        rows, ns = self._env.trace()
+        n = int(ns[self._index])
+        cap = rows.shape[0]
+        if n > cap:
+            raise RuntimeError(f"cycle had {n} samples, trace capacity is {cap}")
+        tr = rows[:n, :, self._index].cpu().numpy()
+        for h, (c0, w) in TRACE_HISTORIES.items():
+            v = tr[:, c0:c0 + w] if w == 3 else tr[:, c0]
+            if h.startswith(("jet_", "drag_", "coriolis_", "added_", "deform_", "acceleration_force")):
+                v = v[1:]          # force histories have no initial entry
+            if h == "state_history":
+                v = v.astype(np.int64)
+            setattr(self, f"{h}_history", v)
+        self.state_history = np.array([self.phase[int(k)] for k in tr[:, 0]])
+        self.asymmetry_torque_history = np.zeros((n - 1, 3))
+        L = tr[:, TRACE["length"]]
+        self.position_front_history = np.stack([L / 2, 0 * L, 0 * L], 1)
+        for h in ("center_of_mass", "center_of_mass_rate", "center_of_mass_acc_rate"):
+            x = getattr(self, f"{h}_history")
+            setattr(self, f"{h}_history", np.stack([x, 0 * x, 0 * x], 1))
+
+    # ----------------------------------------------------------- state views
+    velocity = property(lambda self: self._v("v"))
+    angular_velocity = property(lambda self: self._v("w"))
+    acceleration = property(lambda self: self._v("acc"))
+    angular_acceleration = property(lambda self: self._v("alpha"))
+    euler_angle = property(lambda self: self._v("eta"))
+    position_world = property(lambda self: self._v("pw"))
+    position = property(lambda self: self._v("pos"))
+    angle = property(lambda self: self._v("ang"))
+    prev_position = property(lambda self: self._v("ppos"))
+    prev_angle = property(lambda self: self._v("pang"))
+    avg_cycle_velocity = property(lambda self: self._v("avgv"))
+    avg_cycle_angular_velocity = property(lambda self: self._v("avgw"))
+    cycle_time = property(lambda self: self._f("cycle_time"))
+    time = property(lambda self: self._f("time"))
+    refill_time = property(lambda self: self._f("refill_time"))
+    jet_time = property(lambda self: self._f("jet_time"))
+    coast_time = property(lambda self: self._f("coast_time"))
+    _contract_rate = property(lambda self: self._f("contract_rate"))
+    _release_rate = property(lambda self: self._f("release_rate"))
+    cycle = property(lambda self: int(self._f("cycle")))
+    state = property(lambda self: self.phase[int(self._f("phase"))])
+
+    def _geo(self, name):
+        x = self._f(name)
+        return np.float32(x) if self._f("geom32") else x
+
+    length = property(lambda self: self._geo("length"))
+    width = property(lambda self: self._geo("width"))
+    volume = property(lambda self: self._geo("volume"))
+    contraction = property(lambda self: np.float32(self._f("contraction")) if self._f("contr32")
+                           else self._f("contraction"))
+    prev_water_volume = property(lambda self: np.float32(self._f("prev_volume")) if self._f("pvol32")
+                                 else self._f("prev_volume"))
+    center_of_mass = property(lambda self: np.array([self._f("com"), 0.0, 0.0]))
+    center_of_mass_rate = property(lambda self: np.array([self._f("com_rate"), 0.0, 0.0]))
+    center_of_mass_acc_rate = property(lambda self: np.array([self._f("com_acc"), 0.0, 0.0]))
+    prev_I = property(lambda self: np.diag(self._v("prev_I")))
+
+    @property
+    def velocity_world(self):
+        """R(euler_angle) @ velocity (src/robot.py:866) of the current state."""
+        phi, th, psi = self.euler_angle
+        cp, sp, ct, st, cs, ss = np.cos(phi), np.sin(phi), np.cos(th), np.sin(th), np.cos(psi), np.sin(psi)
+        R = np.array([[cs * ct, cs * st * sp - ss * cp, cs * st * cp + ss * sp],
+                      [ss * ct, ss * st * sp + cs * cp, ss * st * cp - cs * sp],
+                      [-st, ct * sp, ct * cp]])
+        return R @ self.velocity
+
+    def get_cycle_count(self):
+        return self.cycle

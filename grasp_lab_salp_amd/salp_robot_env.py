@@ -1,0 +1,240 @@
+"""Drop-in ``SalpRobotEnv`` (reference: src/salp_robot_env.py:22-670).
+
+Same constructor, spaces, ``reset`` / ``step`` signatures, return types,
+reward, termination and ``info`` keys as the reference's Gymnasium env, so the
+``make_env`` of src/train_robot.py:11-21 runs unchanged with
+``from grasp_lab_salp_amd.salp_robot_env import SalpRobotEnv``.  One env-step
+(one breathing cycle, hundreds of physics ticks) runs as one launch of the
+HIP step kernel on a 1-env :class:`BatchedSalpEnv`; for many envs use
+:class:`~grasp_lab_salp_amd.vec_env.SalpVecEnv`, which runs them all in one
+launch.
+
+Targets and obstacles are drawn on the host from the process-global
+``np.random`` exactly as the reference draws them
+(src/salp_robot_env.py:449-559), then handed to the device: seeding
+``np.random`` reproduces the reference's episodes.
+
+Not on the device (fail loudly): pygame rendering / GIF recording / the
+interactive loop (visualisation, src/salp_robot_env.py:586-1595) and the
+action / observation randomisation and latency options (off in every
+reference script, src/salp_robot_env.py:54-56).
+"""
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+import torch
+
+from ._abi import EPISODE_METRIC_KEYS, INFO, MAX_OBSTACLES, REWARD_COMPONENT_KEYS
+from .batched_env import BatchedSalpEnv
+from .robot import Robot
+from .spaces import Box, GymEnv
+
+__all__ = ["SalpRobotEnv", "draw_target", "draw_obstacles", "TANK_MARGIN", "SCALE"]
+
+TANK_MARGIN = 50          # pixels (src/salp_robot_env.py:42)
+SCALE = 200.0             # pixels per meter (src/salp_robot_env.py:470)
+TARGET_RADIUS = 0.2       # success radius, m (src/salp_robot_env.py:43)
+MIN_CLEAR = 0.5           # obstacle clearance from start and target, m (:543)
+
+
+def _tank(width, height, margin=TANK_MARGIN):
+    return ((-width / 2 + margin) / SCALE, (width / 2 - margin) / SCALE,
+            (-height / 2 + margin) / SCALE, (height / 2 - margin) / SCALE)
+
+
+def draw_target(width, height, strategy="random", current_pos=None, center=None, max_distance=2.0):
+    """generate_target_point (src/salp_robot_env.py:449-533): a float32 [x, y]
+    drawn from the global np.random in the reference's call order, clamped to
+    the tank.  Unknown strategies raise ValueError like the reference."""
+    x_min, x_max, y_min, y_max = _tank(width, height)
+    cur = np.zeros(2) if current_pos is None else np.asarray(current_pos, np.float64)[:2]
+    if strategy == "random":
+        tx = np.random.uniform(x_min, x_max)
+        ty = np.random.uniform(y_min, y_max)
+        target = np.array([tx, ty])
+    elif strategy == "relative":
+        c = cur if center is None else np.asarray(center)
+        dist = np.random.uniform(0.1, max_distance)
+        ang = np.random.uniform(0, 2 * np.pi)
+        target = c + dist * np.array([np.cos(ang), np.sin(ang)])
+    elif strategy == "circle":
+        c = cur if center is None else np.asarray(center)
+        ang = np.random.uniform(0, 2 * np.pi)
+        target = c + max_distance * np.array([np.cos(ang), np.sin(ang)])
+    elif strategy == "corridor":
+        c = cur if center is None else np.asarray(center)
+        target = np.array([np.random.uniform(x_min, x_max), c[1]])
+    else:
+        raise ValueError(f"Unknown target generation strategy: {strategy}")
+    target[0] = np.clip(target[0], x_min, x_max)
+    target[1] = np.clip(target[1], y_min, y_max)
+    return target.astype(np.float32)
+
+
+def draw_obstacles(width, height, num_obstacles, obstacle_radius, target):
+    """_generate_obstacles (src/salp_robot_env.py:535-559): rejection sampling
+    from the global np.random, at most 200 tries per obstacle; the list can
+    come out shorter than num_obstacles."""
+    x_min, x_max, y_min, y_max = _tank(width, height)
+    sep = 2 * obstacle_radius + 0.1
+    placed = []
+    for _ in range(num_obstacles):
+        for _try in range(200):
+            px = np.random.uniform(x_min, x_max)
+            py = np.random.uniform(y_min, y_max)
+            pos = np.array([px, py], dtype=np.float32)
+            ok = np.linalg.norm(pos) > MIN_CLEAR and np.linalg.norm(pos - target) > MIN_CLEAR
+            ok = ok and not any(np.linalg.norm(pos - o) < sep for o in placed)
+            if ok:
+                placed.append(pos)
+                break
+    return placed
+
+
+class SalpRobotEnv(GymEnv):
+    """The reference task env on the device (see module docstring)."""
+
+    metadata = {"render_modes": ["human", "rgb_array"], "render_fps": 60}
+
+    def __init__(self, render_mode: Optional[str] = None, width: int = 900, height: int = 700,
+                 robot: Optional[Robot] = None, num_obstacles: int = 2, obstacle_radius: float = 0.2,
+                 device: Optional[int] = None):
+        if robot is None:
+            raise AttributeError("SalpRobotEnv needs a Robot (the reference fails in reset() without one)")
+        if not 0 <= num_obstacles <= MAX_OBSTACLES:
+            raise ValueError(f"num_obstacles must be in [0, {MAX_OBSTACLES}] on the device")
+        self.width, self.height = width, height
+        self.pos_init = np.array([width / 2, height / 2])
+        self.tank_margin = TANK_MARGIN
+        self.target_radius = TARGET_RADIUS
+        self.num_obstacles = num_obstacles
+        self.obstacle_radius = obstacle_radius
+        self.obstacles = []
+        self.render_mode = render_mode
+        self.action_randomization = False
+        self.observation_randomization = False
+        self.latency = False
+        self.robot = robot
+        self.action = np.array([0.0, 0.0, 0.0])
+        self.prev_action = np.array([0.0, 0.0, 0.0])
+        self.action_space = Box(low=np.array([0.0, 0.0, -1.0]), high=np.array([1.0, 1.0, 1.0]),
+                                dtype=np.float32)
+        obs_dim = 6 + 2 * num_obstacles
+        self.observation_space = Box(low=np.full(obs_dim, -np.inf, dtype=np.float32),
+                                     high=np.full(obs_dim, np.inf, dtype=np.float32), dtype=np.float32)
+        self.np_random = np.random.default_rng()
+        params = robot.salp_params(width=int(width), height=int(height), num_obstacles=int(num_obstacles),
+                                   obstacle_radius=float(obstacle_radius))
+        self._sim = BatchedSalpEnv(1, params=params, device=device)
+        robot._bind(self._sim, 0, owner=self)
+        self._last_obs = None
+        self._last_info = None
+        self.reset()
+
+    # ------------------------------------------------------------ options
+    def enable_action_randomization(self):
+        self.action_randomization = True
+
+    def enable_observation_randomization(self):
+        self.observation_randomization = True
+
+    def enable_latency(self):
+        self.latency = True
+
+    def _unsupported(self):
+        if self.action_randomization or self.observation_randomization or self.latency:
+            raise NotImplementedError("action/observation randomisation and latency "
+                                      "(src/salp_robot_env.py:157-194, 293-297) are not on the device yet")
+
+    # ------------------------------------------------------------ helpers
+    def generate_target_point(self, strategy: str = "random", center=None, max_distance: float = 2.0):
+        cur = self.robot.position_world[:2] if self.robot._bound else None
+        return draw_target(self.width, self.height, strategy, cur, center, max_distance)
+
+    def _generate_obstacles(self):
+        self.obstacles = draw_obstacles(self.width, self.height, self.num_obstacles,
+                                        self.obstacle_radius, self.target_point)
+
+    @staticmethod
+    def _rescale_action(action):
+        """src/salp_robot_env.py:166-174 (the device does the same in float32)."""
+        r = np.zeros_like(action)
+        r[0] = action[0] * 0.06
+        r[1] = action[1] * 10.0
+        r[2] = action[2] * (np.pi / 2)
+        return r
+
+    def sample_random_action(self) -> np.ndarray:
+        return self.action_space.sample().astype(np.float32)
+
+    def get_cycle_count(self) -> int:
+        return self.robot.cycle
+
+    def _obs_len(self):
+        return 6 + 2 * len(self.obstacles)
+
+    def _get_observation(self) -> np.ndarray:
+        """Observation of the current state (src/salp_robot_env.py:651-670),
+        as computed by the last device call."""
+        return self._last_obs.copy()
+
+    def _check_obstacle_collision(self) -> bool:
+        return bool(self._last_info is not None and self._last_info[INFO["hit_obstacle"]] != 0)
+
+    def _calculate_episode_metrics(self) -> Dict[str, float]:
+        row = self._last_info
+        return {k: float(row[INFO[k]]) for k in EPISODE_METRIC_KEYS}
+
+    # ------------------------------------------------------------ gym API
+    def reset(self, seed: Optional[int] = None, options: Optional[Dict] = None) -> Tuple[np.ndarray, Dict]:
+        """src/salp_robot_env.py:114-155.  Like the reference, `seed` only
+        seeds self.np_random; targets and obstacles come from np.random."""
+        if seed is not None:
+            self.np_random = np.random.default_rng(seed)
+        self.target_point = self.generate_target_point(strategy="random")
+        self._generate_obstacles()
+        ob = np.zeros((1, MAX_OBSTACLES, 2), np.float32)
+        for k, o in enumerate(self.obstacles):
+            ob[0, k] = o
+        obs = self._sim.reset_to(self.target_point[None], ob, [len(self.obstacles)])
+        self.prev_action = np.array([0.0, 0.0, 0.0])
+        self.action = np.array([0.0, 0.0, 0.0])
+        self._last_obs = obs[0, :self._obs_len()].cpu().numpy()
+        self._last_info = None
+        self.robot._clear_history()
+        return self._get_observation(), {}
+
+    def step(self, action: np.ndarray) -> Tuple[np.ndarray, float, bool, bool, Dict]:
+        """src/salp_robot_env.py:196-299: one breathing cycle on the device."""
+        self._unsupported()
+        a = np.asarray(action, dtype=np.float32).reshape(3)   # SB3 passes the Box dtype
+        self.action = a.copy()
+        record = self.robot.record
+        if record and self._sim._trace is None:
+            self._sim.enable_trace(Robot._trace_capacity())
+        elif not record and self._sim._trace is not None:
+            self._sim.disable_trace()
+        r = self._sim.step(torch.from_numpy(a[None]), auto_reset=False, want_terminal_obs=False)
+        packed = torch.cat([r.obs[0].double(), r.reward, r.terminated.double(), r.truncated.double(),
+                            r.info[0]]).cpu().numpy()
+        od = self._sim.obs_dim
+        obs = packed[:od].astype(np.float32)[:self._obs_len()]
+        reward, done, truncated = float(packed[od]), bool(packed[od + 1]), bool(packed[od + 2])
+        self._last_obs = obs
+        self._last_info = packed[od + 3:]
+        if record:
+            self.robot._load_history()
+        info = {"position_history": self.robot.position_world_history,
+                "length_history": self.robot.length_history,
+                "width_history": self.robot.width_history}
+        info.update({k: float(self._last_info[INFO[k]]) for k in REWARD_COMPONENT_KEYS})
+        if done or truncated:
+            info.update(self._calculate_episode_metrics())
+        self.prev_action = self.action
+        return obs.copy(), reward, done, truncated, info
+
+    def render(self):
+        raise NotImplementedError("rendering (pygame, src/salp_robot_env.py:1198-1258) is out of scope")
+
+    def close(self):
+        self._sim.close()

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define SALP_ABI_VERSION 1
+#define SALP_ABI_VERSION 2
 
 #define SALP_MAX_OBSTACLES 4
 #define SALP_OBS_DIM_MAX (6 + 2 * SALP_MAX_OBSTACLES)
@@ -136,12 +136,55 @@ int salp_rollout(SalpEnv* h, int64_t tick_budget, const SalpRolloutBuffers* buf,
  * env-steps (one full cycle each) with auto-reset.  rewards_out [n] = sum. */
 int salp_step_random(SalpEnv* h, int32_t n_steps, double* reward_sum_out, void* stream);
 
+/* ------------------------------------------------ Robot / Nozzle level */
+/* The reference's Robot API for callers that drive the robot directly,
+ * without the task env (src/compare_trajectories.py:120-168,
+ * src/robot.py:1103-1158): per env, in the reference's call order
+ *   nozzle.set_yaw_angle(yaw); nozzle.solve_angles()   -> salp_nozzle_solve
+ *   robot.set_control(contraction, coast_time, angles)  -> salp_robot_set_control
+ *   robot.step_through_cycle()                          -> salp_robot_step_through_cycle
+ * Python floats are float64; the *_f32 flags say that the argument is an
+ * np.float32 instead (NumPy 2 then computes some of the geometry in float32,
+ * as on the env path).  All arrays are device pointers with n_envs rows. */
+/* Robot.reset() (src/robot.py:452-501); mask NULL = all envs */
+int salp_robot_reset(SalpEnv* h, const uint8_t* mask, void* stream);
+/* Nozzle.set_angles(angle1, angle2) (src/robot.py:50-60); angles [n][2] */
+int salp_nozzle_set_angles(SalpEnv* h, const double* angles, void* stream);
+/* Nozzle.set_yaw_angle(yaw) + Nozzle.solve_angles() (src/robot.py:62-98); yaw [n] */
+int salp_nozzle_solve(SalpEnv* h, const double* yaw, int yaw_is_f32, void* stream);
+/* Robot.set_control(contraction, coast_time, [angle1, angle2])
+ * (src/robot.py:544-592); control [n][4] */
+int salp_robot_set_control(SalpEnv* h, const double* control, int contraction_is_f32, void* stream);
+/* Robot.step_through_cycle() (src/robot.py:740-777) */
+int salp_robot_step_through_cycle(SalpEnv* h, void* stream);
+
+/* Per-tick history recording (Robot.enable_history_recording, record=True:
+ * the *_history lists of src/robot.py:687-738).  While a trace buffer is set,
+ * salp_step and salp_robot_step_through_cycle write, for every env, sample 0
+ * (the state before the cycle's first tick) and one sample per tick:
+ *   rows[(t * SALP_TRACE_DIM + col) * n_envs + env],  t < max_samples
+ * n_samples[env] receives the number of samples of the last cycle (ticks + 1;
+ * more than max_samples means the tail was not recorded).  Force columns of
+ * sample 0 are NaN (the reference's force histories are one shorter), and so
+ * are its euler_angle_rate and nozzle_yaw (there the reference holds stale
+ * values left by the previous cycle's last tick).  asymmetry_torque (always
+ * [0, 0, 0.00*|v|] == 0) and position_front (= [length/2, 0, 0]) are not
+ * recorded.  The bench paths (salp_rollout, salp_step_random) never record. */
+typedef struct SalpTraceBuffer {
+    int64_t max_samples;
+    double* rows;          /* [max_samples][SALP_TRACE_DIM][n_envs] */
+    int64_t* n_samples;    /* [n_envs] */
+} SalpTraceBuffer;
+/* buf NULL disables recording; the struct is copied, the arrays are not */
+int salp_set_trace(SalpEnv* h, const SalpTraceBuffer* buf);
+
 /* --------------------------------------------------------- state access */
 /* State is a struct-of-arrays of SALP_NUM_FIELDS fp64 rows of n_envs each:
  * state[field * n_envs + env].  Integer and float32 quantities are stored
  * exactly as doubles. */
 int salp_num_fields(void);
 const char* salp_field_name(int field);
+int salp_trace_dim(void);   /* SALP_TRACE_DIM */
 int salp_get_state(SalpEnv* h, double* state_out, void* stream);
 int salp_set_state(SalpEnv* h, const double* state_in, void* stream);
 /* Diagnostic: n_ticks physics ticks on every env with no env-step boundaries
@@ -180,8 +223,13 @@ enum SalpField {
     /* cycle (src/robot.py:311-322) */
     SALP_F_CYCLE_TIME, SALP_F_TIME, SALP_F_REFILL_TIME, SALP_F_JET_TIME, SALP_F_COAST_TIME,
     SALP_F_CONTRACTION, SALP_F_CONTRACT_RATE, SALP_F_RELEASE_RATE, SALP_F_PHASE, SALP_F_CYCLE,
+    /* 1 if `contraction` is an np.float32 (always on the env path, where it
+     * comes from the float32 action; 0 for a Python float passed to
+     * Robot.set_control): selects float32 vs float64 body geometry */
+    SALP_F_CONTR32,
     /* nozzle (src/robot.py:30-44) */
-    SALP_F_ANGLE1, SALP_F_ANGLE2, SALP_F_YAW, SALP_F_PREV_YAW, SALP_F_TURN_TIME,
+    SALP_F_ANGLE1, SALP_F_ANGLE2, SALP_F_PREV_ANGLE1, SALP_F_PREV_ANGLE2,
+    SALP_F_YAW, SALP_F_PREV_YAW, SALP_F_TURN_TIME,
     /* env (src/salp_robot_env.py:114-155) */
     SALP_F_TARGET0, SALP_F_TARGET1,
     SALP_F_OBST0, SALP_F_OBST_END = SALP_F_OBST0 + 2 * SALP_MAX_OBSTACLES - 1,
@@ -207,6 +255,41 @@ enum SalpInfo {
     SALP_INFO_AVG_R_TIME, SALP_INFO_AVG_R_SIDESLIP, SALP_INFO_AVG_R_OBSTACLE,
     SALP_INFO_EP_RETURN, SALP_INFO_EP_LEN, SALP_INFO_HAS_METRICS, SALP_INFO_HIT_OBSTACLE
 };
+
+/* trace columns (src/robot.py:687-738 history names without "_history") */
+enum SalpTraceCol {
+    SALP_T_STATE = 0,                                   /* phase value */
+    SALP_T_PW0, SALP_T_PW1, SALP_T_PW2,                 /* position_world */
+    SALP_T_V0, SALP_T_V1, SALP_T_V2,                    /* velocity */
+    SALP_T_ACC0, SALP_T_ACC1, SALP_T_ACC2,              /* acceleration */
+    SALP_T_ETA0, SALP_T_ETA1, SALP_T_ETA2,              /* euler_angle */
+    SALP_T_ETAR0, SALP_T_ETAR1, SALP_T_ETAR2,           /* euler_angle_rate */
+    SALP_T_W0, SALP_T_W1, SALP_T_W2,                    /* angular_velocity */
+    SALP_T_ALPHA0, SALP_T_ALPHA1, SALP_T_ALPHA2,        /* angular_acceleration */
+    SALP_T_LENGTH, SALP_T_WIDTH,
+    SALP_T_AREA0, SALP_T_AREA1, SALP_T_AREA2,
+    SALP_T_VOLUME, SALP_T_MASS, SALP_T_MASS_RATE,       /* mass[0,0], mass_rate[0,0] */
+    SALP_T_NOZZLE_YAW,                                  /* nozzle.current_yaw */
+    SALP_T_I0, SALP_T_I1, SALP_T_I2,                    /* inertia_tensor (diag) */
+    SALP_T_TCD0, SALP_T_TCD1, SALP_T_TCD2,              /* trans_drag_coefficient */
+    SALP_T_RCD0, SALP_T_RCD1, SALP_T_RCD2,              /* rot_drag_coefficient */
+    SALP_T_COM, SALP_T_COM_RATE, SALP_T_COM_ACC,        /* x components (y, z == 0) */
+    SALP_T_FRONT_W0, SALP_T_FRONT_W1, SALP_T_FRONT_W2,  /* position_front_world */
+    /* force values (NaN in sample 0) */
+    SALP_T_JETV0, SALP_T_JETV1, SALP_T_JETV2,           /* jet_velocity */
+    SALP_T_JETF0, SALP_T_JETF1, SALP_T_JETF2,           /* jet_force */
+    SALP_T_JETT0, SALP_T_JETT1, SALP_T_JETT2,           /* jet_torque */
+    SALP_T_DRAGF0, SALP_T_DRAGF1, SALP_T_DRAGF2,        /* drag_force */
+    SALP_T_DRAGT0, SALP_T_DRAGT1, SALP_T_DRAGT2,        /* drag_torque */
+    SALP_T_CORF0, SALP_T_CORF1, SALP_T_CORF2,           /* coriolis_force */
+    SALP_T_CORT0, SALP_T_CORT1, SALP_T_CORT2,           /* coriolis_torque */
+    SALP_T_AMF0, SALP_T_AMF1, SALP_T_AMF2,              /* added_mass_force */
+    SALP_T_AMT0, SALP_T_AMT1, SALP_T_AMT2,              /* added_mass_torque */
+    SALP_T_DEFT0, SALP_T_DEFT1, SALP_T_DEFT2,           /* deform_torque */
+    SALP_T_ACCF0, SALP_T_ACCF1, SALP_T_ACCF2,           /* acceleration_force */
+    SALP_TRACE_DIM
+};
+#define SALP_T_FIRST_FORCE SALP_T_JETV0
 
 #ifdef __cplusplus
 }

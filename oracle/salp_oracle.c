@@ -147,15 +147,22 @@ static void nozzle_set_angles(Nozzle* n, double a1, double a2) {
     n->turn_time = nozzle_turn_time(n);
     nozzle_rotation_matrices(n);
 }
-/* src/robot.py:62-69 (yaw is a float32 value) */
+/* src/robot.py:62-69 */
 static void nozzle_set_yaw_angle(Nozzle* n, double yaw) { n->prev_yaw = n->yaw; n->yaw = yaw; }
-/* src/robot.py:71-98 */
-static void nozzle_solve_angles(Nozzle* n) {
+/* src/robot.py:71-98; yaw32: the yaw is an np.float32 (env path), so np.cos /
+ * np.sin run in float32 */
+static void nozzle_solve_angles(Nozzle* n, int yaw32) {
     n->prev_angle1 = n->angle1;
     n->prev_angle2 = n->angle2;
-    float sy, cy;
-    sm_np_sincosf((float)n->yaw, &sy, &cy);         /* np.cos/np.sin of a float32 */
-    V3 td = vneg(v3((double)cy, (double)sy, 0.0));   /* -np.array([cos, sin, 0]) */
+    double sy, cy;
+    if (yaw32) {
+        float s, c;
+        sm_np_sincosf((float)n->yaw, &s, &c);        /* np.cos/np.sin of a float32 */
+        sy = s; cy = c;
+    } else {
+        sm_sincos(n->yaw, &sy, &cy);
+    }
+    V3 td = vneg(v3(cy, sy, 0.0));                   /* -np.array([cos, sin, 0]) */
     td = mTvec(n->R_br, td);                         /* R_br.transpose() @ td */
     double val2 = 2.0 * td.v[2] - 1.0;
     if (val2 < -1.0) val2 = -1.0;
@@ -211,6 +218,7 @@ typedef struct {
     double trans_range[3][2], rot_range[3][2];
     /* control src/robot.py:311-316 */
     double contraction, contract_rate, release_rate, refill_time, jet_time, coast_time;
+    int c32; /* contraction is an np.float32 (env path) rather than a Python float */
     int phase, cycle;
     double time, cycle_time;
     /* dynamic properties; g32: length/width/area/volume/water_mass/mass are
@@ -242,33 +250,37 @@ typedef struct {
 } Obj;
 
 /* ------------------------------------------------ geometry.py restated */
-/* src/geometry.py:14-15, 25-26 (compression is a float32 value: **2 is float32) */
-static double poly_time(double c32, const double* k) {
-    float sq = (float)c32 * (float)c32;
-    return k[0] * (double)sq + k[1] * c32 + k[2];
+/* src/geometry.py:14-15, 25-26.  c32: the compression is an np.float32 (env
+ * path), so compression**2 is float32; a Python float squares in float64. */
+static double poly_time(double c, int c32, const double* k) {
+    double sq = c32 ? (double)((float)c * (float)c) : c * c;
+    return k[0] * sq + k[1] * c + k[2];
 }
-/* src/geometry.py:39-50 */
+/* src/geometry.py:39-50; with an np.float32 contraction (c32) `L0 - c` is a
+ * py float - np.float32 = np.float32 */
 static double compute_length(int st, double ct, double refill, double turn, double L0, double c,
-                             double cr, double rr, int* is32) {
+                             double cr, double rr, int c32, int* is32) {
     *is32 = 0;
+    double Lc = c32 ? (double)((float)L0 - (float)c) : L0 - c;
     if (st == REFILL) {
         if (ct < refill) return L0 - ct * cr;
-        *is32 = 1;
-        return (double)((float)L0 - (float)c);              /* py float - np.float32 */
+        *is32 = c32;
+        return Lc;
     }
-    if (st == JET) return (double)((float)L0 - (float)c) + (ct - pymax(refill, turn)) * rr;
+    if (st == JET) return Lc + (ct - pymax(refill, turn)) * rr;
     return L0;
 }
 /* src/geometry.py:53-64 */
 static double compute_width(int st, double ct, double refill, double turn, double W0, double c,
-                            double cr, double rr, int* is32) {
+                            double cr, double rr, int c32, int* is32) {
     *is32 = 0;
+    double Wc = c32 ? (double)((float)W0 + (float)c) : W0 + c;
     if (st == REFILL) {
         if (ct < refill) return W0 + ct * cr;
-        *is32 = 1;
-        return (double)((float)W0 + (float)c);
+        *is32 = c32;
+        return Wc;
     }
-    if (st == JET) return (double)((float)W0 + (float)c) - (ct - pymax(refill, turn)) * rr;
+    if (st == JET) return Wc - (ct - pymax(refill, turn)) * rr;
     return W0;
 }
 /* src/geometry.py:67-75 */
@@ -445,11 +457,11 @@ static V3 r_jet_moment_arm(const Obj* o) {
 /* src/robot.py:1028-1038 */
 static double r_current_length(const Obj* o, int* is32) {
     return compute_length(o->phase, o->cycle_time, o->refill_time, o->nz.turn_time, o->init_length,
-                          o->contraction, o->contract_rate, o->release_rate, is32);
+                          o->contraction, o->contract_rate, o->release_rate, o->c32, is32);
 }
 static double r_current_width(const Obj* o, int* is32) {
     return compute_width(o->phase, o->cycle_time, o->refill_time, o->nz.turn_time, o->init_width,
-                         o->contraction, o->contract_rate, o->release_rate, is32);
+                         o->contraction, o->contract_rate, o->release_rate, o->c32, is32);
 }
 static V3 r_trans_cd(const Obj* o) {
     return compute_drag_coefficient(o->length, o->width, o->init_length, o->init_width,
@@ -610,14 +622,16 @@ static void robot_reset(Obj* o) {
 }
 
 /* src/robot.py:544-592 (dynamics_randomization off) */
-static void robot_set_control(Obj* o, double contraction, double coast_time, double a1, double a2) {
+static void robot_set_control(Obj* o, double contraction, double coast_time, double a1, double a2,
+                              int c32) {
     o->avg_v = vzero(); o->avg_w = vzero();
     o->contraction = contraction; o->coast_time = coast_time;
+    o->c32 = c32;
     nozzle_set_angles(&o->nz, a1, a2);
     o->cycle += 1;
     o->cycle_time = 0.0;
-    o->refill_time = poly_time(o->contraction, REFILL_C);
-    o->jet_time = poly_time(o->contraction, PROPUL_C);
+    o->refill_time = poly_time(o->contraction, c32, REFILL_C);
+    o->jet_time = poly_time(o->contraction, c32, PROPUL_C);
     o->contract_rate = o->refill_time > 0 ? o->contraction / o->refill_time : 0.0;
     o->release_rate = o->jet_time > 0 ? o->contraction / o->jet_time : 0.0;
 }
@@ -719,15 +733,62 @@ static void robot_step(Obj* o) {
     robot_update_state(o);
     robot_update_properties(o);
 }
-/* src/robot.py:740-757; returns the tick count */
-static int64_t robot_step_through_cycle(Obj* o) {
+/* One history sample (src/robot.py:687-738) in the SalpTraceCol layout of
+ * include/salp.h, column col at rec[col * rs].  first: sample 0 of a cycle
+ * (force values, euler_angle_rate and nozzle yaw are NaN there). */
+static void robot_record(Obj* o, double* rec, int64_t rs, int first) {
+#define PUT(c, x) rec[(int64_t)(c) * rs] = (x)
+#define PUT3(c, vec) do { V3 v_ = (vec); PUT(c, v_.v[0]); PUT((c) + 1, v_.v[1]); PUT((c) + 2, v_.v[2]); } while (0)
+    PUT(SALP_T_STATE, o->phase);
+    PUT3(SALP_T_PW0, o->pw); PUT3(SALP_T_V0, o->v); PUT3(SALP_T_ACC0, o->acc);
+    PUT3(SALP_T_ETA0, o->eta); PUT3(SALP_T_W0, o->w); PUT3(SALP_T_ALPHA0, o->alpha);
+    PUT(SALP_T_LENGTH, o->length); PUT(SALP_T_WIDTH, o->width);
+    PUT3(SALP_T_AREA0, o->area);
+    PUT(SALP_T_VOLUME, o->volume);
+    PUT(SALP_T_MASS, o->mass.m[0][0]);
+    PUT(SALP_T_MASS_RATE, o->mass_rate.m[0][0]);
+    M3 I = r_get_inertia(o);
+    PUT(SALP_T_I0, I.m[0][0]); PUT(SALP_T_I1, I.m[1][1]); PUT(SALP_T_I2, I.m[2][2]);
+    PUT3(SALP_T_TCD0, o->tcd); PUT3(SALP_T_RCD0, o->rcd);
+    PUT(SALP_T_COM, o->com.v[0]); PUT(SALP_T_COM_RATE, o->com_rate.v[0]);
+    PUT(SALP_T_COM_ACC, o->com_acc.v[0]);
+    /* get_front_position_world_frame (src/robot.py:924-928) */
+    PUT3(SALP_T_FRONT_W0, to_world_frame(o->eta, v3(o->length / 2, 0.0, 0.0)));
+    if (first) {
+        for (int k = SALP_T_FIRST_FORCE; k < SALP_TRACE_DIM; ++k) PUT(k, NAN);
+        PUT(SALP_T_ETAR0, NAN); PUT(SALP_T_ETAR1, NAN); PUT(SALP_T_ETAR2, NAN);
+        PUT(SALP_T_NOZZLE_YAW, NAN);
+        return;
+    }
+    PUT3(SALP_T_ETAR0, o->eta_rate);
+    PUT(SALP_T_NOZZLE_YAW, o->nz.current_yaw);
+    PUT3(SALP_T_JETV0, o->jet_velocity); PUT3(SALP_T_JETF0, o->jet_force);
+    PUT3(SALP_T_JETT0, o->jet_torque); PUT3(SALP_T_DRAGF0, o->drag_force);
+    PUT3(SALP_T_DRAGT0, o->drag_torque); PUT3(SALP_T_CORF0, o->coriolis_force);
+    PUT3(SALP_T_CORT0, o->coriolis_torque); PUT3(SALP_T_AMF0, o->added_mass_force);
+    PUT3(SALP_T_AMT0, o->added_mass_torque); PUT3(SALP_T_DEFT0, o->deform_torque);
+    PUT3(SALP_T_ACCF0, o->acceleration_force);
+#undef PUT3
+#undef PUT
+}
+
+/* src/robot.py:740-777; returns the tick count.  rows != NULL: record
+ * (record=True), sample t of this env at rows + t * SALP_TRACE_DIM * rs. */
+static int64_t robot_step_through_cycle(Obj* o, double* rows, int64_t rs, int64_t max_samples,
+                                        int64_t* n_samples) {
     double total = pymax(o->refill_time, o->nz.turn_time) + o->jet_time + o->coast_time;
     o->avg_v = vdivs(vsub(o->pos, o->ppos), total);
     o->avg_w = vdivs(vsub(o->ang, o->pang), total);
     o->ppos = o->pos;
     o->pang = o->ang;
+    if (rows && max_samples > 0) robot_record(o, rows, rs, 1);
     int64_t n = 0;
-    while (o->cycle_time < total) { robot_step(o); ++n; }
+    while (o->cycle_time < total) {
+        robot_step(o);
+        ++n;
+        if (rows && n < max_samples) robot_record(o, rows + n * SALP_TRACE_DIM * rs, rs, 0);
+    }
+    if (n_samples) *n_samples = n + 1;
     return n;
 }
 
@@ -830,9 +891,9 @@ static int64_t env_begin_and_run_cycle(Obj* o, const float* action) {
     float r[3];
     env_rescale_action(action, r);
     nozzle_set_yaw_angle(&o->nz, (double)r[2]);
-    nozzle_solve_angles(&o->nz);
-    robot_set_control(o, (double)r[0], (double)r[1], o->nz.angle1, o->nz.angle2);
-    return robot_step_through_cycle(o);
+    nozzle_solve_angles(&o->nz, 1);
+    robot_set_control(o, (double)r[0], (double)r[1], o->nz.angle1, o->nz.angle2, 1);
+    return robot_step_through_cycle(o, NULL, 0, 0, NULL);
 }
 
 /* src/salp_robot_env.py:349-397 */
@@ -970,8 +1031,11 @@ static void obj_pack(const Obj* o, double* s, int64_t n, int64_t i) {
     F(s, SALP_F_RELEASE_RATE, n, i) = o->release_rate;
     F(s, SALP_F_PHASE, n, i) = o->phase;
     F(s, SALP_F_CYCLE, n, i) = o->cycle;
+    F(s, SALP_F_CONTR32, n, i) = o->c32;
     F(s, SALP_F_ANGLE1, n, i) = o->nz.angle1;
     F(s, SALP_F_ANGLE2, n, i) = o->nz.angle2;
+    F(s, SALP_F_PREV_ANGLE1, n, i) = o->nz.prev_angle1;
+    F(s, SALP_F_PREV_ANGLE2, n, i) = o->nz.prev_angle2;
     F(s, SALP_F_YAW, n, i) = o->nz.yaw;
     F(s, SALP_F_PREV_YAW, n, i) = o->nz.prev_yaw;
     F(s, SALP_F_TURN_TIME, n, i) = o->nz.turn_time;
@@ -1043,8 +1107,11 @@ static void obj_unpack(Obj* o, const SalpParams* p, const double* s, int64_t n, 
     o->release_rate = F(s, SALP_F_RELEASE_RATE, n, i);
     o->phase = (int)F(s, SALP_F_PHASE, n, i);
     o->cycle = (int)F(s, SALP_F_CYCLE, n, i);
+    o->c32 = (int)F(s, SALP_F_CONTR32, n, i);
     o->nz.angle1 = F(s, SALP_F_ANGLE1, n, i);
     o->nz.angle2 = F(s, SALP_F_ANGLE2, n, i);
+    o->nz.prev_angle1 = F(s, SALP_F_PREV_ANGLE1, n, i);
+    o->nz.prev_angle2 = F(s, SALP_F_PREV_ANGLE2, n, i);
     o->nz.yaw = F(s, SALP_F_YAW, n, i);
     o->nz.prev_yaw = F(s, SALP_F_PREV_YAW, n, i);
     o->nz.turn_time = F(s, SALP_F_TURN_TIME, n, i);
@@ -1215,8 +1282,8 @@ int64_t oracle_robot_trace(const SalpParams* p, const float* actions, int n_acti
         float r[3];
         env_rescale_action(actions + 3 * c, r);
         nozzle_set_yaw_angle(&o.nz, (double)r[2]);
-        nozzle_solve_angles(&o.nz);
-        robot_set_control(&o, (double)r[0], (double)r[1], o.nz.angle1, o.nz.angle2);
+        nozzle_solve_angles(&o.nz, 1);
+        robot_set_control(&o, (double)r[0], (double)r[1], o.nz.angle1, o.nz.angle2, 1);
         double total = pymax(o.refill_time, o.nz.turn_time) + o.jet_time + o.coast_time;
         o.avg_v = vdivs(vsub(o.pos, o.ppos), total);
         o.avg_w = vdivs(vsub(o.ang, o.pang), total);
@@ -1240,6 +1307,63 @@ int64_t oracle_robot_trace(const SalpParams* p, const float* actions, int n_acti
         }
     }
     return row;
+}
+
+/* Robot / Nozzle level (include/salp.h salp_robot_*, salp_nozzle_*). */
+int oracle_robot_reset(const SalpParams* p, int64_t n, double* state, const uint8_t* mask) {
+    for (int64_t i = 0; i < n; ++i) {
+        if (mask && !mask[i]) continue;
+        Obj o;
+        obj_unpack(&o, p, state, n, i);
+        robot_reset(&o);
+        o.pending = 0;
+        obj_pack(&o, state, n, i);
+    }
+    return 0;
+}
+int oracle_nozzle_set_angles(const SalpParams* p, int64_t n, double* state, const double* ang) {
+    for (int64_t i = 0; i < n; ++i) {
+        Obj o;
+        obj_unpack(&o, p, state, n, i);
+        nozzle_set_angles(&o.nz, ang[2 * i], ang[2 * i + 1]);
+        obj_pack(&o, state, n, i);
+    }
+    return 0;
+}
+int oracle_nozzle_solve(const SalpParams* p, int64_t n, double* state, const double* yaw, int yaw32) {
+    for (int64_t i = 0; i < n; ++i) {
+        Obj o;
+        obj_unpack(&o, p, state, n, i);
+        nozzle_set_yaw_angle(&o.nz, yaw[i]);
+        nozzle_solve_angles(&o.nz, yaw32);
+        obj_pack(&o, state, n, i);
+    }
+    return 0;
+}
+int oracle_robot_set_control(const SalpParams* p, int64_t n, double* state, const double* ctl, int c32) {
+    for (int64_t i = 0; i < n; ++i) {
+        Obj o;
+        obj_unpack(&o, p, state, n, i);
+        robot_set_control(&o, ctl[4 * i], ctl[4 * i + 1], ctl[4 * i + 2], ctl[4 * i + 3], c32);
+        obj_pack(&o, state, n, i);
+    }
+    return 0;
+}
+/* step_through_cycle for every env; rows/n_samples may be NULL (no record).
+ * ticks_out [n] may be NULL. */
+int oracle_robot_cycle(const SalpParams* p, int64_t n, double* state, double* rows,
+                       int64_t max_samples, int64_t* n_samples, int64_t* ticks_out) {
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int64_t i = 0; i < n; ++i) {
+        Obj o;
+        obj_unpack(&o, p, state, n, i);
+        int64_t t = robot_step_through_cycle(&o, rows ? rows + i : NULL, n, max_samples,
+                                             n_samples ? n_samples + i : NULL);
+        o.pending = 0;
+        if (ticks_out) ticks_out[i] = t;
+        obj_pack(&o, state, n, i);
+    }
+    return 0;
 }
 
 /* Math self-test rows, same layout as salp_math_selftest (host side). */

@@ -25,8 +25,13 @@ Fixture files (all ``np.savez_compressed``):
                    target/obstacle draws recorded in the post-reset snapshot.
 ``tick_trace.npz`` robot-level per-tick histories (``record=True``,
                    src/robot.py:740-777) for a few cycles.
+``robot_trace.npz`` the bare-robot call sequence of src/compare_trajectories.py:
+                   142-150 / src/robot.py:1149-1155 with Python-float controls
+                   (float64 geometry throughout), per-tick histories and the
+                   robot state after every cycle, for the canonical robot and
+                   the demo robot of src/robot.py:1104-1107.
 
-Usage:  python tests/golden/make_golden.py  [--jobs 8]
+Usage:  python tests/golden/make_golden.py  [--jobs 8] [--only robot]
 """
 import argparse
 import multiprocessing as mp
@@ -303,6 +308,94 @@ def run_trace_job(job):
     return res
 
 
+HIST_KEYS = ["position_world_history", "velocity_history", "acceleration_history",
+             "euler_angle_history", "euler_angle_rate_history", "angular_velocity_history",
+             "angular_acceleration_history", "length_history", "width_history", "area_history",
+             "volume_history", "mass_history", "mass_rate_history", "nozzle_yaw_history",
+             "inertia_tensor_history", "trans_drag_coefficient_history",
+             "rot_drag_coefficient_history", "center_of_mass_history",
+             "center_of_mass_rate_history", "center_of_mass_acc_rate_history",
+             "position_front_world_history", "jet_velocity_history", "jet_force_history",
+             "jet_torque_history", "drag_force_history", "drag_torque_history",
+             "coriolis_force_history", "coriolis_torque_history", "added_mass_force_history",
+             "added_mass_torque_history", "deform_torque_history", "asymmetry_torque_history",
+             "acceleration_force_history", "state_history"]
+FORCE_KEYS = ("jet_", "drag_", "coriolis_", "added_", "deform_", "asymmetry_", "acceleration_force")
+ROBOT_STATE = ["velocity", "angular_velocity", "acceleration", "angular_acceleration", "euler_angle",
+               "position_world", "position", "angle", "prev_position", "prev_angle",
+               "avg_cycle_velocity", "avg_cycle_angular_velocity"]
+ROBOT_SCAL = ["length", "width", "volume", "prev_water_volume", "cycle_time", "time", "refill_time",
+              "jet_time", "coast_time", "contraction", "_contract_rate", "_release_rate"]
+
+
+def run_robot_job(job):
+    """Bare robot driven with Python-float controls (float64 geometry)."""
+    ref_robot, _ = _import_reference()
+    c = job["robot"]
+    nozzle = ref_robot.Nozzle(length1=c["length1"], length2=c["length2"], length3=c["length3"],
+                              area=c["area"], mass=c["nozzle_mass"])
+    robot = ref_robot.Robot(dry_mass=c["dry_mass"], init_length=c["init_length"],
+                            init_width=c["init_width"], max_contraction=c["max_contraction"],
+                            nozzle=nozzle)
+    robot.nozzle.set_angles(angle1=0.0, angle2=0.0)
+    robot.set_environment(density=c["density"])
+    robot.enable_history_recording()
+    robot.reset()
+    hist = {k: [] for k in HIST_KEYS}
+    cyc, end = [], {}
+    for i, (contraction, coast, yaw) in enumerate(job["controls"]):
+        if i == job.get("reset_at", -1):
+            robot.reset()
+        robot.nozzle.set_yaw_angle(yaw_angle=float(yaw))
+        robot.nozzle.solve_angles()
+        robot.set_control(contraction=float(contraction), coast_time=float(coast),
+                          nozzle_angles=np.array([robot.nozzle.angle1, robot.nozzle.angle2]))
+        robot.step_through_cycle()
+        n = len(robot.length_history)
+        for k in HIST_KEYS:
+            v = getattr(robot, k)
+            if k == "state_history":
+                v = [s.value for s in v]
+            elif k in ("mass_history", "mass_rate_history"):
+                v = [np.asarray(x, np.float64).reshape(-1)[0] for x in v]
+            elif k == "inertia_tensor_history":
+                v = [np.asarray(x, np.float64).reshape(3) for x in v]
+            v = np.asarray(v, np.float64)
+            if k.startswith(FORCE_KEYS):
+                v = np.concatenate([np.full((1,) + v.shape[1:], np.nan), v], 0)
+            hist[k].append(v)
+        cyc.append(np.full(n, i))
+        for k in ROBOT_STATE:
+            end.setdefault("end_" + k, []).append(np.array(getattr(robot, k), np.float64).reshape(3))
+        for k in ROBOT_SCAL:
+            end.setdefault("end_" + k, []).append(np.float64(getattr(robot, k)))
+        end.setdefault("end_center_of_mass", []).append(np.float64(robot.center_of_mass[0]))
+        end.setdefault("end_prev_I", []).append(np.diag(robot.prev_I).astype(np.float64))
+        end.setdefault("end_phase", []).append(np.int64(robot.state.value))
+        end.setdefault("end_cycle", []).append(np.int64(robot.cycle))
+        for k in ("angle1", "angle2", "prev_angle1", "prev_angle2", "yaw", "prev_yaw", "turn_time"):
+            end.setdefault("end_n_" + k, []).append(np.float64(getattr(robot.nozzle, k)))
+    res = {k: np.concatenate(v, 0) for k, v in hist.items()}
+    res["cycle_id"] = np.concatenate(cyc)
+    res.update({k: np.asarray(v) for k, v in end.items()})
+    res["controls"] = np.asarray(job["controls"], np.float64)
+    res["reset_at"] = np.int64(job.get("reset_at", -1))
+    return res
+
+
+# the demo robot of src/robot.py:1104-1107
+DEMO = dict(length1=0.052, length2=0.039, length3=0.031, area=np.pi * 0.01 ** 2, nozzle_mass=0.440,
+            dry_mass=0.756, init_length=0.26, init_width=0.14, max_contraction=0.04, density=1000)
+ROBOT_JOBS = [
+    # src/robot.py:1149-1152: contraction 0.03, coast 2, yaw 0 (Python floats)
+    dict(name="canon", robot=CANON, controls=[(0.03, 2.0, 0.0), (0.03, 2.0, 0.0),
+                                              (0.05, 0.5, 0.7), (0.012, 0.3, -1.2),
+                                              (0.06, 1.0, 1.5707963267948966)], reset_at=4),
+    dict(name="demo", robot=DEMO, controls=[(0.03, 2.0, 0.0), (0.04, 1.0, -0.4),
+                                            (0.02, 0.2, 0.9), (0.035, 0.7, -1.5)]),
+]
+
+
 def build_jobs():
     jobs = [dict(seed=0, kind="fixed", n_steps=40)]
     for s in range(1, 17):
@@ -330,7 +423,21 @@ def build_jobs():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=8)
+    ap.add_argument("--only", choices=["robot"], default=None)
     args = ap.parse_args()
+    ctx = mp.get_context("fork")
+    with ctx.Pool(args.jobs) as pool:
+        robots = pool.map(run_robot_job, ROBOT_JOBS, chunksize=1)
+    out = {}
+    for job, res in zip(ROBOT_JOBS, robots):
+        for k, v in res.items():
+            out[f"{job['name']}/{k}"] = v
+        for k, v in job["robot"].items():
+            out[f"{job['name']}/param_{k}"] = np.float64(v)
+    np.savez_compressed(os.path.join(OUT_DIR, "robot_trace.npz"), **out)
+    if args.only == "robot":
+        print("robot trace samples", {j["name"]: len(r["cycle_id"]) for j, r in zip(ROBOT_JOBS, robots)})
+        return
     jobs = build_jobs()
     ctx = mp.get_context("fork")
     with ctx.Pool(args.jobs) as pool:

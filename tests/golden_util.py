@@ -17,6 +17,7 @@ SCAL_MAP = {"length": "r_length", "width": "r_width", "volume": "r_volume",
             "coast_time": "r_coast_time", "contraction": "r_contraction",
             "contract_rate": "r__contract_rate", "release_rate": "r__release_rate",
             "phase": "r_phase", "cycle": "r_cycle", "angle1": "n_angle1", "angle2": "n_angle2",
+            "prev_angle1": "n_prev_angle1", "prev_angle2": "n_prev_angle2",
             "yaw": "n_yaw", "prev_yaw": "n_prev_yaw", "turn_time": "n_turn_time",
             "n_obst": "e_n_obstacles", "prev_dist": "e_prev_dist", "ep_len": "e_ep_len",
             "path_len": "e_path_length", "sum_a0": "e_sum_a0",
@@ -58,6 +59,8 @@ def snapshot_to_state(d, prefix, rows):
     for i in range(3):
         s[FIELD[f"prev_I{i}"]] = pI[:, i]
     s[FIELD["geom32"]] = g("r_len_is_f32")
+    # env path: set_control always receives the float32 rescaled action
+    s[FIELD["contr32"]] = 1.0
     s[FIELD["pvol32"]] = g("r_pvol_is_f32")
     t = g("e_target")
     s[FIELD["target0"]], s[FIELD["target1"]] = t[:, 0], t[:, 1]

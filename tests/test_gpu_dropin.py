@@ -1,0 +1,271 @@
+"""The drop-in layer on the device: Robot/Nozzle-level ABI, per-tick recording,
+SalpRobotEnv and the SB3-shaped SalpVecEnv.
+
+Device results must equal the oracle bit for bit (the oracle is pinned to the
+reference by test_oracle_golden.py / test_robot_api_oracle.py) and, where a
+reference fixture exists, match it within the tolerances stated there.
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import load_episodes, load_trace
+from grasp_lab_salp_amd._abi import FIELD, INFO, TRACE, TRACE_DIM, default_params
+from grasp_lab_salp_amd.batched_env import BatchedSalpEnv
+from grasp_lab_salp_amd.robot import Nozzle, Robot
+from grasp_lab_salp_amd.salp_robot_env import SalpRobotEnv
+from grasp_lab_salp_amd.vec_env import SalpVecEnv, make_vec_env
+from oracle.oracle import Oracle
+from test_robot_api_oracle import (JOBS, OracleSim, compare_to_reference, drive, job_params,
+                                   load_robot_fixture)
+
+pytestmark = pytest.mark.gpu
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+class DeviceSim:
+    """BatchedSalpEnv behind the OracleSim method names used by drive()."""
+
+    def __init__(self, params, n=1):
+        self.env = BatchedSalpEnv(n, params=params)
+        self.n = n
+        self.cap = None
+
+    def get_state_np(self):
+        return _np(self.env.get_state())
+
+    def robot_reset(self, mask=None):
+        self.env.robot_reset(mask)
+
+    def nozzle_solve(self, yaw, f32):
+        self.env.nozzle_solve(np.asarray(yaw, np.float64), f32)
+
+    def robot_set_control(self, ctl, f32):
+        self.env.robot_set_control(np.asarray(ctl, np.float64), f32)
+
+    def robot_cycle(self, max_samples=0):
+        if max_samples and self.cap != max_samples:
+            self.env.enable_trace(max_samples)
+            self.cap = max_samples
+        self.env.robot_step_through_cycle()
+        if not max_samples:
+            return None, None, None
+        rows, ns = self.env.trace()
+        return None, _np(rows), _np(ns)
+
+
+def assert_state_equal(g, o, what=""):
+    bad = [k for k in range(g.shape[0]) if not np.array_equal(g[k], o[k], equal_nan=True)]
+    assert not bad, f"{what}: fields differ {bad[:8]}"
+
+
+@pytest.mark.parametrize("name", JOBS)
+def test_robot_api_bit_identical_to_oracle_and_matches_reference(name):
+    d = load_robot_fixture()
+    p = job_params(d, name)
+    rows_d, ends_d = drive(DeviceSim(p), d, name)
+    o = OracleSim(p, 1)
+    o.reset()          # the device env was built by salp_create (constructor + env reset)
+    rows_o, ends_o = drive(o, d, name)
+    assert rows_d.shape == rows_o.shape
+    assert np.array_equal(rows_d, rows_o, equal_nan=True)
+    assert np.array_equal(ends_d, ends_o, equal_nan=True)
+    compare_to_reference(rows_d, ends_d, d, name)
+
+
+def test_batched_robot_api_random_controls():
+    """512 robots, random Python-float and float32 controls, several cycles,
+    with and without recording: state and traces equal to the oracle."""
+    n, rng = 512, np.random.default_rng(7)
+    p = default_params()
+    dev, ora = DeviceSim(p, n), OracleSim(p, n)
+    ora.reset()
+    dev.robot_reset()
+    ora.robot_reset()
+    for cyc in range(4):
+        f32 = cyc % 2 == 1
+        yaw = rng.uniform(-np.pi / 2, np.pi / 2, n)
+        c = rng.uniform(0, 0.06, n)
+        coast = rng.uniform(0, 3, n)
+        if f32:
+            yaw, c, coast = (x.astype(np.float32).astype(np.float64) for x in (yaw, c, coast))
+        dev.nozzle_solve(yaw, f32)
+        ora.nozzle_solve(yaw, f32)
+        st = ora.state
+        ctl = np.stack([c, coast, st[FIELD["angle1"]], st[FIELD["angle2"]]], 1)
+        dev.robot_set_control(ctl, f32)
+        ora.robot_set_control(ctl, f32)
+        ms = 1600 if cyc >= 2 else 0
+        _, rd, nd = dev.robot_cycle(ms)
+        _, ro, no = ora.robot_cycle(ms)
+        assert_state_equal(dev.get_state_np(), ora.state, f"cycle {cyc}")
+        if ms:
+            assert np.array_equal(nd, no)
+            for i in range(0, n, 37):
+                k = int(no[i])
+                assert np.array_equal(rd[:k, :, i], ro[:k, :, i], equal_nan=True), (cyc, i)
+
+
+def test_env_step_with_recording_equals_robot_trace():
+    """salp_step with a trace buffer records the same samples as the oracle's
+    robot-level cycle with the float32 controls of _rescale_action, and the
+    recorded step leaves the same state as an unrecorded one."""
+    t = load_trace()
+    p = default_params()
+    a = BatchedSalpEnv(1, params=p, seed=1)
+    b = BatchedSalpEnv(1, params=p, seed=1)
+    o = OracleSim(p, 1)
+    o.state[:] = _np(a.get_state())
+    a.enable_trace(1600)
+    for act in t["actions"]:
+        act = np.asarray(act, np.float32)
+        a.step(torch.tensor(act[None]))
+        b.step(torch.tensor(act[None]))
+        r = act * np.float32(0.06), act * np.float32(10.0), act * np.float32(np.pi / 2)
+        o.nozzle_solve([float(r[2][2])], True)
+        o.robot_set_control([[float(r[0][0]), float(r[1][1]), o.state[FIELD["angle1"], 0],
+                              o.state[FIELD["angle2"], 0]]], True)
+        _, ro, no = o.robot_cycle(1600)
+        rows, ns = a.trace()
+        k = int(no[0])
+        assert int(_np(ns)[0]) == k
+        assert np.array_equal(_np(rows)[:k, :, 0], ro[:k, :, 0], equal_nan=True)
+        ga, gb = _np(a.get_state()), _np(b.get_state())
+        for f in ("pw0", "pw1", "v0", "eta2", "length", "cycle_time", "phase", "turn_time"):
+            assert np.array_equal(ga[FIELD[f]], gb[FIELD[f]]), f
+            assert np.array_equal(ga[FIELD[f]], o.state[FIELD[f]]), f
+
+
+def _make_env(**kw):
+    nozzle = Nozzle(length1=0.05, length2=0.05, length3=0.05, area=0.00016, mass=1.0)
+    robot = Robot(dry_mass=1.0, init_length=0.3, init_width=0.15, max_contraction=0.06, nozzle=nozzle)
+    robot.nozzle.set_angles(angle1=0.0, angle2=0.0)
+    robot.set_environment(density=1000)
+    return SalpRobotEnv(render_mode=None, robot=robot, **kw)
+
+
+@pytest.mark.parametrize("job", [0, 3, 17, 21, 22])
+def test_salp_robot_env_reproduces_reference_episodes(job):
+    """make_env + np.random.seed(seed) + reset + the fixture's actions: the
+    drop-in env redraws the reference's targets/obstacles itself and must
+    follow the reference's episode (obs 1e-5 relative, same flags) — the
+    whole episode free-running, resets included."""
+    d = load_episodes()
+    rows = np.where(d["job_index"] == job)[0]
+    K = int(d["num_obstacles_cfg"][rows[0]])
+    seed = job if job <= 16 else 101 + (job - 17)
+    np.random.seed(seed)
+    env = _make_env(num_obstacles=K)
+    obs, info = env.reset()
+    assert info == {}
+    assert np.array_equal(env.target_point, d["b_e_target"][rows[0]])
+    od = 6 + 2 * K
+    for r in rows:
+        obs, rew, term, trunc, info = env.step(d["action"][r])
+        assert obs.dtype == np.float32 and obs.shape == (od,)
+        ref = d["obs"][r][:od]
+        assert np.max(np.abs(obs - ref) / np.maximum(np.abs(ref), 1e-3)) <= 1e-5, r
+        assert abs(rew - d["reward"][r]) <= 1e-4
+        assert (term, trunc) == (bool(d["terminated"][r]), bool(d["truncated"][r]))
+        assert set(info) >= {"position_history", "rewards/track", "rewards/obstacle"}
+        if term or trunc:
+            assert "path_length" in info and "avg_rewards_track" in info
+            obs, _ = env.reset()
+            assert np.array_equal(env.target_point, d["r_e_target"][r])
+    env.close()
+
+
+def test_salp_robot_env_robot_views_and_recording():
+    env = _make_env()
+    env.robot.enable_history_recording()
+    obs, rew, term, trunc, info = env.step(np.array([0.8, 0.1, 0.3], np.float32))
+    ph = info["position_history"]
+    assert len(ph) == len(env.robot.length_history) > 1
+    assert np.array_equal(ph[-1], env.robot.position_world)
+    assert env.robot.cycle == 1
+    assert env.robot.state in Robot.phase and env.robot.cycle_time > 0
+    assert len(env.robot.jet_force_history) == len(ph) - 1
+    env.close()
+
+
+def test_standalone_robot_class_matches_fixture():
+    """compare_trajectories.simulate_trajectory's call sequence on the drop-in
+    Robot (Python-float controls), record=True."""
+    d = load_robot_fixture()
+    name = "canon"
+    c = lambda k: float(d[f"{name}/param_{k}"])
+    nozzle = Nozzle(length1=c("length1"), length2=c("length2"), length3=c("length3"), area=c("area"),
+                    mass=c("nozzle_mass"))
+    robot = Robot(dry_mass=c("dry_mass"), init_length=c("init_length"), init_width=c("init_width"),
+                  max_contraction=c("max_contraction"), nozzle=nozzle)
+    robot.nozzle.set_angles(angle1=0.0, angle2=0.0)
+    robot.set_environment(density=c("density"))
+    robot.enable_history_recording()
+    robot.reset()
+    cid = d[f"{name}/cycle_id"]
+    for i, (con, coast, yaw) in enumerate(d[f"{name}/controls"]):
+        if i == int(d[f"{name}/reset_at"]):
+            robot.reset()
+        robot.nozzle.set_yaw_angle(yaw_angle=float(yaw))
+        robot.nozzle.solve_angles()
+        robot.set_control(contraction=float(con), coast_time=float(coast),
+                          nozzle_angles=np.array([robot.nozzle.angle1, robot.nozzle.angle2]))
+        robot.step_through_cycle()
+        m = cid == i
+        ref = d[f"{name}/position_world_history"][m]
+        got = robot.position_world_history
+        assert got.shape == ref.shape
+        assert np.max(np.abs(got[:, :2] - ref[:, :2])) <= 1e-9
+        assert np.array_equal(robot.length_history, d[f"{name}/length_history"][m])
+        assert [s.value for s in robot.state_history] == list(d[f"{name}/state_history"][m])
+
+
+def test_vec_env_semantics_against_oracle():
+    """SB3 VecEnv contract: auto-reset, terminal_observation, TimeLimit.truncated,
+    Monitor episode stats; obs / rewards / dones equal to the oracle's."""
+    n = 256
+    venv = SalpVecEnv(n, seed=3)
+    o = Oracle(default_params(), n, seed=3)
+    o.reset()
+    obs = venv.reset()
+    assert np.array_equal(obs, o.reset())
+    rng = np.random.default_rng(0)
+    ep_ret = np.zeros(n)
+    ep_len = np.zeros(n, int)
+    seen_done = 0
+    for t in range(40):
+        a = np.stack([rng.uniform(0, 1, n), rng.uniform(0, 1, n) * 0.3, rng.uniform(-1, 1, n)],
+                     1).astype(np.float32)
+        obs, rew, dones, infos = venv.step(a)
+        ro = o.step(a, auto_reset=True)
+        assert obs.dtype == np.float32 and rew.dtype == np.float32 and dones.dtype == bool
+        # (random actions can hit the reference's own blow-up: NaN states)
+        assert np.array_equal(obs, ro["obs"], equal_nan=True)
+        assert np.array_equal(rew, ro["reward"].astype(np.float32), equal_nan=True)
+        assert np.array_equal(dones, (ro["terminated"] | ro["truncated"]).astype(bool))
+        ep_ret += ro["reward"]
+        ep_len += 1
+        for i in np.nonzero(dones)[0]:
+            seen_done += 1
+            inf = infos[i]
+            assert np.array_equal(inf["terminal_observation"], ro["terminal_obs"][i], equal_nan=True)
+            assert inf["TimeLimit.truncated"] == bool(ro["truncated"][i] and not ro["terminated"][i])
+            assert inf["episode"]["l"] == ep_len[i]
+            assert abs(inf["episode"]["r"] - ep_ret[i]) <= 1e-5 or np.isnan(ep_ret[i])
+            assert "final_distance" in inf
+            ep_ret[i], ep_len[i] = 0.0, 0
+        for i in np.nonzero(~dones)[0][:5]:
+            assert "episode" not in infos[i] and "rewards/track" in infos[i]
+    assert seen_done > 0
+
+
+def test_make_vec_env_from_reference_make_env():
+    venv = make_vec_env(_make_env, n_envs=64, seed=5)
+    assert venv.num_envs == 64 and venv.observation_space.shape == (10,)
+    obs = venv.reset()
+    r = venv.step_tensors(torch.rand(64, 3, device="cuda"))
+    assert r.obs.shape == (64, 10) and obs.shape == (64, 10)
+    venv.close()

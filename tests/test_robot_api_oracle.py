@@ -1,0 +1,187 @@
+"""The oracle's Robot-level path against the reference (tests/golden/robot_trace.npz).
+
+robot_trace.npz holds the bare-robot call sequence of
+src/compare_trajectories.py:142-150 / src/robot.py:1149-1155 run by the
+reference with Python-float controls (so every geometry quantity is float64),
+with record=True per-tick histories (src/robot.py:687-738) and the robot
+state after every cycle, for the canonical robot (src/train_robot.py:13-17)
+and the demo robot of src/robot.py:1104-1107 (make_golden.py, ROBOT_JOBS).
+
+Tolerances:
+* phases, tick counts (history lengths): exact;
+* in-plane quantities (x, y, yaw and what derives from them):
+  |err| <= 1e-5 * max(|ref|, 1e-3 * max|ref|) — north_star's 1e-5 bar (the
+  rotational rates, which cross zero every cycle, with 1e-2 * max|ref|).  The
+  canonical robot is bit-identical on >97% of samples; the residue comes from
+  NumPy's float64 arccos / arcsin / arctan2 (SVML here), whose 1-ulp
+  differences the nozzle IK amplifies (arcsin near +-1) into ~1e-8 relative
+  changes of the turn time on the demo robot's yaw=0.9 cycle;
+* out-of-plane channels (z, roll, pitch and the torques about x/y) are pure
+  rounding noise of the nozzle direction's z component (1e-8 .. 1e-33):
+  absolute 1e-6.
+"""
+import numpy as np
+import pytest
+
+from golden_util import GOLDEN
+from grasp_lab_salp_amd._abi import FIELD, TRACE, TRACE_HISTORIES, default_params
+from oracle.oracle import Oracle
+
+REL_TOL = 1e-5
+FLOOR = 1e-3
+# rotational rates cross zero every cycle: relative to 1% of their range
+RATE_FLOOR = 1e-2
+RATES = {"euler_angle_rate", "angular_velocity", "angular_acceleration"}
+OOP_ATOL = 1e-6
+OUT_OF_PLANE = {
+    ("position_world", 2), ("velocity", 2), ("acceleration", 2), ("euler_angle", 0),
+    ("euler_angle", 1), ("euler_angle_rate", 0), ("euler_angle_rate", 1),
+    ("angular_velocity", 0), ("angular_velocity", 1), ("angular_acceleration", 0),
+    ("angular_acceleration", 1), ("position_front_world", 2), ("jet_velocity", 2),
+    ("jet_force", 2), ("jet_torque", 0), ("jet_torque", 1), ("drag_force", 2),
+    ("drag_torque", 0), ("drag_torque", 1), ("coriolis_force", 2), ("coriolis_torque", 0),
+    ("coriolis_torque", 1), ("coriolis_torque", 2), ("added_mass_force", 2),
+    ("added_mass_torque", 0), ("added_mass_torque", 1), ("deform_torque", 0),
+    ("deform_torque", 1), ("acceleration_force", 2)}
+JOBS = ("canon", "demo")
+
+
+def load_robot_fixture():
+    return dict(np.load(f"{GOLDEN}/robot_trace.npz"))
+
+
+def job_params(d, name):
+    g = lambda k: float(d[f"{name}/param_{k}"])
+    return default_params(nozzle_length1=g("length1"), nozzle_length2=g("length2"),
+                          nozzle_length3=g("length3"), nozzle_area=g("area"),
+                          nozzle_mass=g("nozzle_mass"), dry_mass=g("dry_mass"),
+                          init_length=g("init_length"), init_width=g("init_width"),
+                          max_contraction=g("max_contraction"), density=g("density"))
+
+
+def drive(sim, d, name, max_samples=2000):
+    """Run a fixture job's call sequence on `sim` (the Oracle, or the device
+    through the same method names); returns (trace rows [samples, DIM], end
+    states [cycles, NUM_FIELDS])."""
+    controls = d[f"{name}/controls"]
+    reset_at = int(d[f"{name}/reset_at"])
+    sim.robot_reset()
+    rows, ends = [], []
+    for i, (c, coast, yaw) in enumerate(controls):
+        if i == reset_at:
+            sim.robot_reset()
+        sim.nozzle_solve([yaw], False)
+        st = sim.get_state_np()
+        sim.robot_set_control([[c, coast, st[FIELD["angle1"], 0], st[FIELD["angle2"], 0]]], False)
+        _, tr, ns = sim.robot_cycle(max_samples)
+        rows.append(tr[:int(ns[0]), :, 0])
+        ends.append(sim.get_state_np()[:, 0].copy())
+    return np.concatenate(rows, 0), np.array(ends)
+
+
+class OracleSim(Oracle):
+    def get_state_np(self):
+        return self.state
+
+
+def compare_to_reference(rows, ends, d, name):
+    cid = d[f"{name}/cycle_id"]
+    assert rows.shape[0] == len(cid), "history lengths (tick counts) differ"
+    assert np.array_equal(rows[:, TRACE["state"]], d[f"{name}/state_history"])
+    for h, (c0, w) in TRACE_HISTORIES.items():
+        ref = d[f"{name}/{h}_history"]
+        ref = ref[:, None] if ref.ndim == 1 else ref
+        for k in range(w):
+            got, r = rows[:, c0 + k], ref[:, k]
+            m = ~np.isnan(got)
+            if h in ("nozzle_yaw", "euler_angle_rate"):
+                # sample 0 of a cycle holds a stale value in the reference
+                assert np.array_equal(~m, np.r_[True, cid[1:] != cid[:-1]])
+            else:
+                assert np.array_equal(np.isnan(got), np.isnan(r)), (h, k)
+            got, r = got[m], r[m]
+            if (h, k) in OUT_OF_PLANE:
+                assert np.max(np.abs(got - r), initial=0) <= OOP_ATOL, (h, k)
+            else:
+                mx = np.max(np.abs(r), initial=0)
+                fl = RATE_FLOOR if h in RATES else FLOOR
+                e = np.abs(got - r) / np.maximum(np.abs(r), fl * mx + 1e-300)
+                assert np.max(e, initial=0) <= REL_TOL, (h, k, float(np.max(e)))
+    # histories the layout leaves out are what the header says they are
+    asym = d[f"{name}/asymmetry_torque_history"]
+    assert np.all(asym[~np.isnan(asym)] == 0)
+    assert np.all(d[f"{name}/center_of_mass_history"][:, 1:] == 0)
+    # end-of-cycle state
+    for k in ("length", "width", "volume", "cycle_time", "time", "refill_time", "jet_time",
+              "coast_time", "contraction"):
+        ref = d[f"{name}/end_{k}"]
+        assert np.max(np.abs(ends[:, FIELD[k]] - ref) / np.maximum(np.abs(ref), 1e-12)) <= REL_TOL, k
+    assert np.array_equal(ends[:, FIELD["phase"]], d[f"{name}/end_phase"])
+    assert np.array_equal(ends[:, FIELD["cycle"]], d[f"{name}/end_cycle"])
+    for k in ("angle1", "angle2", "prev_angle1", "prev_angle2", "turn_time"):
+        ref = d[f"{name}/end_n_{k}"]
+        assert np.max(np.abs(ends[:, FIELD[k]] - ref)) <= 1e-7, k
+    for k, f in (("position_world", "pw"), ("velocity", "v"), ("avg_cycle_velocity", "avgv")):
+        ref = d[f"{name}/end_{k}"]
+        for c in (0, 1):
+            got = ends[:, FIELD[f"{f}{c}"]]
+            mx = np.max(np.abs(ref[:, c]))
+            assert np.max(np.abs(got - ref[:, c]) / np.maximum(np.abs(ref[:, c]), FLOOR * mx)) <= REL_TOL
+
+
+@pytest.fixture(scope="module")
+def fixture():
+    return load_robot_fixture()
+
+
+@pytest.mark.parametrize("name", JOBS)
+def test_oracle_robot_path_matches_reference(fixture, name):
+    o = OracleSim(job_params(fixture, name), 1)
+    rows, ends = drive(o, fixture, name)
+    compare_to_reference(rows, ends, fixture, name)
+
+
+def test_canonical_robot_path_mostly_bit_identical(fixture):
+    o = OracleSim(job_params(fixture, "canon"), 1)
+    rows, _ = drive(o, fixture, "canon")
+    for h in ("position_world", "velocity", "length", "width", "volume", "mass", "jet_force"):
+        c0, w = TRACE_HISTORIES[h]
+        ref = fixture[f"canon/{h}_history"]
+        ref = ref[:, None] if ref.ndim == 1 else ref
+        assert np.mean(rows[:, c0:c0 + w] == ref[:, :w]) > 0.97, h
+
+
+def test_env_path_full_trace_matches_reference():
+    """tick_trace.npz (env-path float32 controls): the full history layout,
+    including the force histories, from oracle_robot_cycle."""
+    t = dict(np.load(f"{GOLDEN}/tick_trace.npz"))
+    o = OracleSim(default_params(), 1)
+    o.robot_reset()
+    rows = []
+    for a in t["actions"]:
+        r = np.float32(a[0]) * np.float32(0.06), np.float32(a[1]) * np.float32(10.0), \
+            np.float32(a[2]) * np.float32(np.pi / 2)
+        o.nozzle_solve([float(r[2])], True)
+        o.robot_set_control([[float(r[0]), float(r[1]), o.state[FIELD["angle1"], 0],
+                              o.state[FIELD["angle2"], 0]]], True)
+        _, tr, ns = o.robot_cycle(2000)
+        rows.append(tr[:int(ns[0]), :, 0])
+    rows = np.concatenate(rows, 0)
+    assert rows.shape[0] == len(t["cycle_id"])
+    assert np.array_equal(rows[:, TRACE["state"]], t["state_history"])
+    for h in ("jet_velocity", "jet_force", "drag_force", "coriolis_force", "added_mass_force",
+              "acceleration_force", "jet_torque", "drag_torque", "added_mass_torque",
+              "deform_torque", "length", "width", "volume", "mass", "position_world", "velocity"):
+        c0, w = TRACE_HISTORIES[h]
+        ref = t[f"{h}_history"]
+        ref = ref[:, None] if ref.ndim == 1 else ref
+        for k in range(w):
+            got, r = rows[:, c0 + k], ref[:, k]
+            assert np.array_equal(np.isnan(got), np.isnan(r)), (h, k)
+            m = ~np.isnan(r)
+            if (h, k) in OUT_OF_PLANE:
+                assert np.max(np.abs(got[m] - r[m]), initial=0) <= OOP_ATOL, (h, k)
+                continue
+            mx = np.max(np.abs(r[m]), initial=0)
+            e = np.abs(got[m] - r[m]) / np.maximum(np.abs(r[m]), FLOOR * mx + 1e-300)
+            assert np.max(e, initial=0) <= REL_TOL, (h, k, float(np.max(e)))
