@@ -156,7 +156,7 @@ class BatchedSalpEnv:
         self._run(_lib.load().salp_step_random(self._h, int(n_steps), _ptr(rs), self._stream()))
         return rs
 
-    def rollout(self, tick_budget, buffers=None, steps_done=None, max_steps=0, chunk=32):
+    def rollout(self, tick_budget, buffers=None, steps_done=None, max_steps=0, chunk=128):
         """Chained random-action rollout: each env runs ``tick_budget`` physics
         ticks, completing as many env-steps as fit (auto-reset).  ``buffers`` is
         an optional dict of preallocated device tensors {obs [cap,n,obs_dim],

@@ -541,7 +541,7 @@ int salp_rollout(SalpEnv* h, int64_t tick_budget, const SalpRolloutBuffers* buf,
     SalpRolloutBuffers b{};
     if (buf) b = *buf;
     if (b.capacity < 0) return fail(h, SALP_EINVAL, "salp_rollout: capacity < 0");
-    int32_t chunk = b.chunk > 0 ? b.chunk : 32;
+    int32_t chunk = b.chunk > 0 ? b.chunk : 128;
     int64_t n_chunks = (tick_budget + chunk - 1) / chunk;
     RolloutArgs args{h->state, h->dp, n_chunks, chunk, b.max_steps, b};
     hipLaunchKernelGGL(k_rollout, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream, args);

@@ -92,7 +92,7 @@ typedef struct SalpRolloutBuffers {
     int64_t* steps_done;   /* [n_envs] completed env-steps counter (in/out)    */
     int64_t max_steps;     /* >0: a lane starts no env-step once steps_done
                             * reaches it (fixed-length rollouts, n_steps)     */
-    int32_t chunk;         /* ticks between env-step boundaries (0 = 32)      */
+    int32_t chunk;         /* ticks between env-step boundaries (0 = 128)     */
     int32_t reserved;
 } SalpRolloutBuffers;
 

@@ -1,16 +1,19 @@
 #!/bin/bash
 # PMC passes over a short bench run (one counter group per pass, kernel trace
 # only; no sys/runtime trace domains).  Outputs under gpurun_out/pmc_<tag>_*.
+# Each pass is SIGKILLed after 90 s (a counter request the hardware cannot
+# serve hangs rocprofv3, SIGTERM included).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-r1}
 ARGS=${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --no-lockstep}
+PASSES=${PASSES:-fetch write waves mix}
 pass() {  # name counters...
     local name=$1
     shift
     echo "== pmc $name $(date +%T)"
-    timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-trace --output-format csv \
+    timeout -s KILL 90 rocprofv3 --pmc "$@" --kernel-trace --output-format csv \
         -d "gpurun_out/pmc_${TAG}_${name}" -o run -- python3 bench.py $ARGS \
         > "gpurun_out/pmc_${TAG}_${name}.log" 2>&1
     local rc=$?
@@ -18,8 +21,11 @@ pass() {  # name counters...
     tail -n 3 "gpurun_out/pmc_${TAG}_${name}.log"
     if [ $rc -ne 0 ]; then echo "stopping (rc=$rc)"; exit $rc; fi
 }
-pass flops SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP64_TRANS SQ_INSTS_VALU SQ_INSTS_SALU
-pass mix SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64
-pass waves SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE
-pass fetch FETCH_SIZE
-pass write WRITE_SIZE
+for p in $PASSES; do
+    case $p in
+        fetch) pass fetch FETCH_SIZE ;;
+        write) pass write WRITE_SIZE ;;
+        waves) pass waves SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE ;;
+        mix) pass mix SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 ;;
+    esac
+done
