@@ -27,13 +27,27 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from grasp_lab_salp_amd._abi import NUM_FIELDS, default_params  # noqa: E402
+from grasp_lab_salp_amd.shard import env_id_offset, reduce_run  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X fp64 vector spec (half the 157.3 TF fp32 rate)
 STATE_BYTES = NUM_FIELDS * 8
 STEP_OUT_BYTES = 10 * 4 + 3 * 4 + 4 + 1   # obs + action + reward(f32) + done per env-step
-# fp64 flop-equivalents per physics tick, counted on the kernel
-F_TICK = float(os.environ.get("SALP_F_TICK", "0")) or None
+
+
+def pmc_profile(n, budget, chunk):
+    """The committed PMC summary (tools/pmc_summary.py) measured on this exact
+    configuration, if any: HBM traffic and fp64 VALU counts of k_rollout."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json"))):
+        try:
+            s = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if s.get("config") == {"n_envs": n, "tick_budget": budget, "chunk": chunk}:
+            best = (os.path.basename(path), s)
+    return best
 
 
 def parse():
@@ -85,7 +99,8 @@ def main():
 
     from grasp_lab_salp_amd.batched_env import BatchedSalpEnv
     n = a.n_envs
-    env = BatchedSalpEnv(n, params=default_params(), seed=a.seed, env_id_offset=rank * n, device=dev.index)
+    env = BatchedSalpEnv(n, params=default_params(), seed=a.seed, env_id_offset=env_id_offset(rank, n),
+                         device=dev.index)
     cap = a.capacity
     bufs = {"obs": torch.zeros((cap, n, env.obs_dim), dtype=torch.float32, device=dev),
             "actions": torch.zeros((cap, n, 3), dtype=torch.float32, device=dev),
@@ -129,19 +144,12 @@ def main():
         torch.cuda.synchronize()
         lock = 4 * n / (e0.elapsed_time(e1) / 1e3)
 
-    t = torch.tensor([elapsed, float(steps_local), kern_ms, lock or 0.0], dtype=torch.float64, device=dev)
-    if world > 1:
-        mx = t.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = t.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        elapsed, steps_total, kern_ms, lock_total = mx[0].item(), sm[1].item(), mx[2].item(), sm[3].item()
-    else:
-        steps_total, lock_total = float(steps_local), lock
+    elapsed, steps_total, kern_ms, lock_total = reduce_run(elapsed, steps_local, kern_ms, lock, device=dev)
     if rank != 0:
         dist.destroy_process_group()
         return
 
+    prof = pmc_profile(n, a.tick_budget, a.chunk)
     ticks_total = float(-(-a.tick_budget // a.chunk) * a.chunk) * n * a.steps * world
     steps_per_launch = steps_local / a.steps
     bytes_launch = n * (2 * STATE_BYTES + 16) + steps_per_launch * STEP_OUT_BYTES
@@ -167,17 +175,21 @@ def main():
         "mean_ticks_per_env_step": ticks_total / max(steps_total, 1.0),
         "kernel_ms_per_launch": kern_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": prof[1]["derived"].get("hbm_bytes") if prof else None,
+                     "traffic_source": prof[0] if prof else None,
                      "bytes_per_launch": bytes_launch,
                      "note": "algorithmic bytes = n*(2*state+16) + env-steps*57 per launch; the "
                              "kernel is fp64-VALU bound (see roofline_valu)"},
         "lockstep_env_steps_per_sec": lock_total,
     }
-    if F_TICK:
-        fl = F_TICK * float(a.tick_budget) * n / (kern_ms / 1e3) / 1e12
+    f_tick = prof[1]["derived"].get("fp64_flops_per_env_tick") if prof else None
+    if f_tick:
+        # executed fp64 flops (PMC, FMA = 2) per env-tick of budget x this run's kernel time
+        fl = f_tick * float(a.tick_budget) * n / (kern_ms / 1e3) / 1e12
         res["roofline_valu"] = {"bound": "fp64-valu", "achieved": fl, "peak": FP64_VALU_PEAK_TFLOPS,
                                 "unit": "TFLOP/s", "frac": fl / FP64_VALU_PEAK_TFLOPS,
-                                "flops_per_tick": F_TICK}
+                                "flops_per_env_tick": f_tick, "source": prof[0]}
     if world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(a.cpu_baseline_seconds)
     print(json.dumps(res), flush=True)

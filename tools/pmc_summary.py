@@ -1,0 +1,70 @@
+"""Summarise the rocprofv3 PMC passes of tools/gpu_pmc.sh for one kernel.
+
+    python tools/pmc_summary.py TAG [--kernel k_rollout] [--n-envs N --tick-budget T --chunk C]
+
+Reads gpurun_out/pmc_<TAG>_<pass>/run_counter_collection.csv and writes
+profiles/<TAG>_pmc_summary.json: per-dispatch means of every counter, the HBM
+bytes per dispatch (FETCH_SIZE and WRITE_SIZE are KiB; FETCH_SIZE doubled, the
+gfx950 correction of MI355X_MICROARCH.md §HBM) and fp64 VALU counts.  bench.py
+reports `roofline.traffic` from the summary whose config matches its own.
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("--kernel", default="k_rollout")
+    ap.add_argument("--n-envs", type=int, default=65536)
+    ap.add_argument("--tick-budget", type=int, default=8192)
+    ap.add_argument("--chunk", type=int, default=128)
+    a = ap.parse_args()
+    per = {}
+    for path in sorted(glob.glob(os.path.join(ROOT, "gpurun_out", f"pmc_{a.tag}_*", "run_counter_collection.csv"))):
+        agg = collections.defaultdict(list)
+        for r in csv.DictReader(open(path)):
+            if a.kernel in r["Kernel_Name"]:
+                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for k, v in agg.items():
+            # the first dispatch is the warm-up launch: keep the timed ones
+            vv = v[1:] if len(v) > 1 else v
+            per[k] = {"mean": sum(vv) / len(vv), "dispatches": len(vv)}
+    if not per:
+        raise SystemExit(f"no counters for {a.kernel} under gpurun_out/pmc_{a.tag}_*")
+    g = lambda k: per[k]["mean"] if k in per else None  # noqa: E731
+    out = {"tag": a.tag, "kernel": a.kernel,
+           "config": {"n_envs": a.n_envs, "tick_budget": a.tick_budget, "chunk": a.chunk},
+           "command": "tools/gpu_pmc.sh: rocprofv3 --pmc <group> --kernel-trace -- python3 bench.py "
+                      "--steps 2 --warmup 1 --no-cpu-baseline --no-lockstep, one pass per group",
+           "per_dispatch": per, "derived": {}}
+    d = out["derived"]
+    if g("FETCH_SIZE") is not None:
+        d["fetch_bytes"] = g("FETCH_SIZE") * 1024 * 2
+    if g("WRITE_SIZE") is not None:
+        d["write_bytes"] = g("WRITE_SIZE") * 1024
+    if "fetch_bytes" in d and "write_bytes" in d:
+        d["hbm_bytes"] = d["fetch_bytes"] + d["write_bytes"]
+    f64 = [g(k) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                          "SQ_INSTS_VALU_TRANS_F64")]
+    if None not in f64:
+        d["fp64_valu_insts"] = sum(f64)
+        d["fp64_flops"] = 64 * (f64[0] + f64[1] + 2 * f64[2] + f64[3])
+        d["fp64_flops_per_env_tick"] = d["fp64_flops"] / (a.n_envs * a.tick_budget)
+    if g("SQ_WAVES"):
+        d["valu_insts_per_wave"] = g("SQ_INSTS_VALU") / g("SQ_WAVES")
+        d["wait_any_frac"] = g("SQ_WAIT_ANY") / g("SQ_WAVE_CYCLES")
+        d["active_valu_frac"] = g("SQ_ACTIVE_INST_VALU") / g("SQ_WAVE_CYCLES")
+    dst = os.path.join(ROOT, "profiles", f"{a.tag}_pmc_summary.json")
+    json.dump(out, open(dst, "w"), indent=1)
+    print(json.dumps(d, indent=1))
+
+
+if __name__ == "__main__":
+    main()
