@@ -332,7 +332,18 @@ struct Hot {
     bool g32, pv32, c32;
 };
 
-#define SF(f) S[(size_t)(f) * (size_t)P.n + (size_t)i]
+/* State access.  The env-step functions below are templates over the state
+ * they read and write: the struct-of-arrays buffer in HBM (double*), or a
+ * register copy of one env's row (ColdRegs*, the rollout boundary) so that the
+ * env-step epilogue/prologue issues all its loads at once instead of one
+ * dependent HBM round trip per read-modify-write. */
+struct ColdRegs { double v[SALP_NUM_FIELDS]; };
+SD double& sref(double* S, const Params& P, int64_t i, int f) { return S[(size_t)f * (size_t)P.n + (size_t)i]; }
+SD const double& sref(const double* S, const Params& P, int64_t i, int f) {
+    return S[(size_t)f * (size_t)P.n + (size_t)i];
+}
+SD double& sref(ColdRegs* C, const Params&, int64_t, int f) { return C->v[f]; }
+#define SF(f) sref(S, P, i, (f))
 
 /* Register-resident values derived from the stored state: geometry of the
  * current body and sin/cos of roll and pitch. */
@@ -570,7 +581,8 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
 /* Nozzle.set_yaw_angle + Nozzle.solve_angles (src/robot.py:62-98).  yaw32:
  * the yaw is an np.float32 (env path, src/salp_robot_env.py:207), so np.cos /
  * np.sin run in float32; otherwise in float64. */
-SD void nozzle_solve(double* S, const Params& P, int64_t i, double yaw, bool yaw32) {
+template <class ST>
+SD void nozzle_solve(ST S, const Params& P, int64_t i, double yaw, bool yaw32) {
     SF(SALP_F_PREV_YAW) = SF(SALP_F_YAW);
     SF(SALP_F_YAW) = yaw;
     SF(SALP_F_PREV_ANGLE1) = SF(SALP_F_ANGLE1);
@@ -610,7 +622,8 @@ SD void nozzle_solve(double* S, const Params& P, int64_t i, double yaw, bool yaw
 }
 
 /* Nozzle.set_angles -> _nozzle_turn_time (src/robot.py:50-60, 173-185) */
-SD double nozzle_set_angles(double* S, const Params& P, int64_t i, double a1, double a2) {
+template <class ST>
+SD double nozzle_set_angles(ST S, const Params& P, int64_t i, double a1, double a2) {
     SF(SALP_F_ANGLE1) = a1;
     SF(SALP_F_ANGLE2) = a2;
     const double turn = fabs(a1 - SF(SALP_F_PREV_ANGLE1)) / P.angle_speed +
@@ -621,7 +634,8 @@ SD double nozzle_set_angles(double* S, const Params& P, int64_t i, double a1, do
 
 /* Robot.set_control (src/robot.py:544-592, geometry.py:14-26); c32: the
  * contraction is an np.float32 (contraction**2 is then float32). */
-SD void set_control(Hot& h, double* S, const Params& P, int64_t i, double contraction, double coast,
+template <class ST>
+SD void set_control(Hot& h, ST S, const Params& P, int64_t i, double contraction, double coast,
                     double a1, double a2, bool c32) {
     SF(SALP_F_AVGV0) = 0.0; SF(SALP_F_AVGV1) = 0.0; SF(SALP_F_AVGV2) = 0.0;
     SF(SALP_F_AVGW0) = 0.0; SF(SALP_F_AVGW1) = 0.0; SF(SALP_F_AVGW2) = 0.0;
@@ -642,7 +656,8 @@ SD void set_control(Hot& h, double* S, const Params& P, int64_t i, double contra
 
 /* Robot.step_through_cycle prologue (src/robot.py:740-748): the previous
  * cycle's displacement over this cycle's total time. */
-SD void cycle_prologue(const Hot& h, double* S, const Params& P, int64_t i) {
+template <class ST>
+SD void cycle_prologue(const Hot& h, ST S, const Params& P, int64_t i) {
     const double total = h.b2;
     double pq0 = SF(SALP_F_PPOS0), pq1 = SF(SALP_F_PPOS1), pq2 = SF(SALP_F_PPOS2);
     double pg0 = SF(SALP_F_PANG0), pg1 = SF(SALP_F_PANG1), pg2 = SF(SALP_F_PANG2);
@@ -658,7 +673,8 @@ SD void cycle_prologue(const Hot& h, double* S, const Params& P, int64_t i) {
 /* ------------------------------------------------ env-step prologue */
 /* SalpRobotEnv.step up to step_through_cycle's loop (src/salp_robot_env.py:
  * 196-210): float32 action rescale, IK, set_control, cycle prologue. */
-SD void begin_step(Hot& h, double* S, const Params& P, int64_t i, float a0, float a1, float a2,
+template <class ST>
+SD void begin_step(Hot& h, ST S, const Params& P, int64_t i, float a0, float a1, float a2,
                    Cache32 c32) {
     SF(SALP_F_ACT0) = a0; SF(SALP_F_ACT1) = a1; SF(SALP_F_ACT2) = a2;
     /* _rescale_action in float32 (src/salp_robot_env.py:166-174) */
@@ -671,7 +687,8 @@ SD void begin_step(Hot& h, double* S, const Params& P, int64_t i, float a0, floa
 
 /* Trace sample: the state columns (src/robot.py:687-716) of the current
  * state.  first: sample 0 of a cycle, whose force / rate columns are NaN. */
-SD void record_state(const Hot& h, const Params& P, const double* S, int64_t i, double* rec,
+template <class ST>
+SD void record_state(const Hot& h, const Params& P, ST S, int64_t i, double* rec,
                      int64_t rs, bool first) {
     auto put = [&](int col, double x) { rec[(int64_t)col * rs] = x; };
     put(SALP_T_STATE, (double)h.phase);
@@ -709,14 +726,16 @@ SD void record_state(const Hot& h, const Params& P, const double* S, int64_t i, 
 }
 
 /* Resume an in-flight cycle: derived per-cycle values from stored ones. */
-SD void resume_cycle(Hot& h, const double* S, const Params& P, int64_t i) {
+template <class ST>
+SD void resume_cycle(Hot& h, ST S, const Params& P, int64_t i) {
     cycle_bounds(h);
     nozzle_direction(SF(SALP_F_ANGLE1), SF(SALP_F_ANGLE2), &h.d0);
 }
 
 /* ------------------------------------------------------ observation */
 /* _get_observation (src/salp_robot_env.py:651-670) */
-SD void observation(const Hot& h, const Rot& R, const double* S, const Params& P, int64_t i,
+template <class ST>
+SD void observation(const Hot& h, const Rot& R, ST S, const Params& P, int64_t i,
                     float* obs) {
     double tx = SF(SALP_F_TARGET0), ty = SF(SALP_F_TARGET1);
     double b0, b1;
@@ -726,7 +745,9 @@ SD void observation(const Hot& h, const Rot& R, const double* S, const Params& P
     obs[2] = (float)h.v0; obs[3] = (float)h.v1;
     obs[4] = (float)h.w2; obs[5] = (float)heading;
     const int nob = (int)SF(SALP_F_N_OBST);
-    for (int k = 0; k < P.num_obstacles; ++k) {
+#pragma unroll
+    for (int k = 0; k < SALP_MAX_OBSTACLES; ++k) {
+        if (k >= P.num_obstacles) break;
         if (k < nob) {
             obs[6 + 2 * k] = (float)(SF(SALP_F_OBST0 + 2 * k) - h.p0);
             obs[7 + 2 * k] = (float)(SF(SALP_F_OBST0 + 2 * k + 1) - h.p1);
@@ -745,7 +766,8 @@ struct StepOut {
 /* ------------------------------------------------ env-step epilogue */
 /* SalpRobotEnv.step after the cycle (src/salp_robot_env.py:237-299), reward
  * (:349-397), collision (:561-568), episode metrics (:399-447). */
-SD StepOut finish_step(const Hot& h, double* S, const Params& P, int64_t i, float* obs,
+template <class ST>
+SD StepOut finish_step(const Hot& h, ST S, const Params& P, int64_t i, float* obs,
                        double* info) {
     StepOut out;
     const Rot R = rot_zyx(h.e0, h.e1, h.e2);
@@ -783,7 +805,9 @@ SD StepOut finish_step(const Hot& h, double* S, const Params& P, int64_t i, floa
     comp[6] = 0.0;
     const int nob = (int)SF(SALP_F_N_OBST);
     double md = 0.0;
-    for (int k = 0; k < nob; ++k) {
+#pragma unroll
+    for (int k = 0; k < SALP_MAX_OBSTACLES; ++k) {
+        if (k >= nob) break;
         double d = np_norm2(px - SF(SALP_F_OBST0 + 2 * k), py - SF(SALP_F_OBST0 + 2 * k + 1));
         if (k == 0 || d < md) md = d;
     }
@@ -800,7 +824,9 @@ SD StepOut finish_step(const Hot& h, double* S, const Params& P, int64_t i, floa
     double thr = l32 ? (double)((float)P.obstacle_radius + (float)Lc / 2.0f)
                      : P.obstacle_radius + Lc / 2;
     bool hit = false;
-    for (int k = 0; k < nob; ++k) {
+#pragma unroll
+    for (int k = 0; k < SALP_MAX_OBSTACLES; ++k) {
+        if (k >= nob) break;
         double d = np_norm2(px - SF(SALP_F_OBST0 + 2 * k), py - SF(SALP_F_OBST0 + 2 * k + 1));
         if (d < thr) hit = true;
     }
@@ -819,6 +845,7 @@ SD StepOut finish_step(const Hot& h, double* S, const Params& P, int64_t i, floa
     const double sa2 = SF(SALP_F_SUM_ABS_A2) + (double)fabsf(a2);
     SF(SALP_F_SUM_A0) = sa0; SF(SALP_F_SUM_A1) = sa1; SF(SALP_F_SUM_ABS_A2) = sa2;
     double sr[7];
+#pragma unroll
     for (int k = 0; k < 7; ++k) {
         sr[k] = SF(SALP_F_SUM_R0 + k) + comp[k];
         SF(SALP_F_SUM_R0 + k) = sr[k];
@@ -892,7 +919,8 @@ SD int draw_reset(const Params& P, uint64_t env_id, uint64_t episode, float* tgt
  * initial shape; the center of mass is taken from the PREVIOUS geometry
  * (get_center_of_mass runs before length/width are reset); nozzle angles are
  * not reset. */
-SD void robot_reset(Hot& h, double* S, const Params& P, int64_t i) {
+template <class ST>
+SD void robot_reset(Hot& h, ST S, const Params& P, int64_t i) {
     h.time = 0.0; h.ct = 0.0; h.phase = REST;
     SF(SALP_F_CYCLE) = 0.0;
     h.v0 = h.v1 = h.v2 = 0.0; h.w0 = h.w1 = h.w2 = 0.0;
@@ -918,9 +946,11 @@ SD void robot_reset(Hot& h, double* S, const Params& P, int64_t i) {
 
 /* SalpRobotEnv.reset with the target / obstacles given (src/salp_robot_env.py:
  * 114-155) -> Robot.reset. */
-SD void reset_env(Hot& h, double* S, const Params& P, int64_t i, const float* tgt,
+template <class ST>
+SD void reset_env(Hot& h, ST S, const Params& P, int64_t i, const float* tgt,
                   const float* obst, int nob, float* obs) {
     SF(SALP_F_TARGET0) = tgt[0]; SF(SALP_F_TARGET1) = tgt[1];
+#pragma unroll
     for (int k = 0; k < SALP_MAX_OBSTACLES; ++k) {
         SF(SALP_F_OBST0 + 2 * k) = k < nob ? (double)obst[2 * k] : 0.0;
         SF(SALP_F_OBST0 + 2 * k + 1) = k < nob ? (double)obst[2 * k + 1] : 0.0;
@@ -938,6 +968,7 @@ SD void reset_env(Hot& h, double* S, const Params& P, int64_t i, const float* tg
     SF(SALP_F_SUM_A0) = 0.0; SF(SALP_F_SUM_A1) = 0.0; SF(SALP_F_SUM_ABS_A2) = 0.0;
     SF(SALP_F_SUM_VEL) = np_norm2(0.0, 0.0);
     SF(SALP_F_INIT_DIST) = dist;
+#pragma unroll
     for (int k = 0; k < 7; ++k) SF(SALP_F_SUM_R0 + k) = 0.0;
     SF(SALP_F_EPISODE) = SF(SALP_F_EPISODE) + 1.0;
     SF(SALP_F_PENDING) = 0.0;
@@ -947,10 +978,71 @@ SD void reset_env(Hot& h, double* S, const Params& P, int64_t i, const float* tg
     }
 }
 
-SD void reset_env_philox(Hot& h, double* S, const Params& P, int64_t i, float* obs) {
+template <class ST>
+SD void reset_env_philox(Hot& h, ST S, const Params& P, int64_t i, float* obs) {
     float tgt[2], obst[2 * SALP_MAX_OBSTACLES];
     int nob = draw_reset(P, (uint64_t)(P.env_offset + i), (uint64_t)SF(SALP_F_EPISODE), tgt, obst);
     reset_env(h, S, P, i, tgt, obst, nob, obs);
+}
+
+/* ------------------------------------- rollout boundary: LDS + registers */
+/* Fields store_hot writes (the tick's state); every other field is "cold":
+ * touched only at env-step boundaries. */
+SD constexpr bool is_hot(int f) {
+    return (f >= SALP_F_V0 && f <= SALP_F_ANG2) || (f >= SALP_F_LENGTH && f <= SALP_F_PVOL32) ||
+           (f >= SALP_F_CYCLE_TIME && f <= SALP_F_PHASE) || f == SALP_F_CONTR32 || f == SALP_F_TURN_TIME;
+}
+/* One env's cold fields into registers with all loads in flight at once. */
+SD void load_cold(ColdRegs& C, const double* S, const Params& P, int64_t i) {
+#pragma unroll
+    for (int f = 0; f < SALP_NUM_FIELDS; ++f)
+        if (!is_hot(f)) C.v[f] = S[(size_t)f * (size_t)P.n + (size_t)i];
+}
+SD void store_cold(const ColdRegs& C, double* S, const Params& P, int64_t i) {
+#pragma unroll
+    for (int f = 0; f < SALP_NUM_FIELDS; ++f)
+        if (!is_hot(f)) S[(size_t)f * (size_t)P.n + (size_t)i] = C.v[f];
+}
+
+/* A lane's slot of a workgroup LDS array [SPILL_N][LANES]: the whole Hot
+ * state (geometry and roll/pitch sin/cos included, so nothing is recomputed
+ * on reload) parks here while the wave runs an env-step boundary. */
+constexpr int SPILL_N = 63;
+struct SpillSlot {
+    double* p;
+    SD_MEMBER double& operator[](int k) const { return p[k * LANES]; }
+};
+SD void spill(const Hot& h, SpillSlot s) {
+    const double v[SPILL_N] = {
+        h.v0, h.v1, h.v2, h.w0, h.w1, h.w2, h.a0, h.a1, h.a2, h.al0, h.al1, h.al2,
+        h.e0, h.e1, h.e2, h.p0, h.p1, h.p2, h.q0, h.q1, h.q2, h.g0, h.g1, h.g2,
+        h.L, h.W, h.V, h.pV, h.com, h.comr, h.coma, h.pI0, h.pI1, h.pI2, h.ct, h.time,
+        h.refill, h.jet, h.coast, h.c, h.cr, h.rr, h.turn, h.d0, h.d1, h.d2, h.sp, h.cp, h.st, h.cth,
+        h.geo.m, h.geo.mr, h.geo.I0, h.geo.I1, h.geo.kc0, h.geo.kc1, h.geo.ra0, h.geo.ra1,
+        h.geo.dimx, h.geo.dimy, h.geo.speed, h.geo.rx,
+        (double)(h.phase | (h.g32 ? 4 : 0) | (h.pv32 ? 8 : 0) | (h.c32 ? 16 : 0))};
+#pragma unroll
+    for (int k = 0; k < SPILL_N; ++k) s[k] = v[k];
+}
+SD void unspill(Hot& h, SpillSlot s) {
+    double v[SPILL_N];
+#pragma unroll
+    for (int k = 0; k < SPILL_N; ++k) v[k] = s[k];
+    h.v0 = v[0]; h.v1 = v[1]; h.v2 = v[2]; h.w0 = v[3]; h.w1 = v[4]; h.w2 = v[5];
+    h.a0 = v[6]; h.a1 = v[7]; h.a2 = v[8]; h.al0 = v[9]; h.al1 = v[10]; h.al2 = v[11];
+    h.e0 = v[12]; h.e1 = v[13]; h.e2 = v[14]; h.p0 = v[15]; h.p1 = v[16]; h.p2 = v[17];
+    h.q0 = v[18]; h.q1 = v[19]; h.q2 = v[20]; h.g0 = v[21]; h.g1 = v[22]; h.g2 = v[23];
+    h.L = v[24]; h.W = v[25]; h.V = v[26]; h.pV = v[27]; h.com = v[28]; h.comr = v[29]; h.coma = v[30];
+    h.pI0 = v[31]; h.pI1 = v[32]; h.pI2 = v[33]; h.ct = v[34]; h.time = v[35];
+    h.refill = v[36]; h.jet = v[37]; h.coast = v[38]; h.c = v[39]; h.cr = v[40]; h.rr = v[41];
+    h.turn = v[42]; h.d0 = v[43]; h.d1 = v[44]; h.d2 = v[45];
+    h.sp = v[46]; h.cp = v[47]; h.st = v[48]; h.cth = v[49];
+    h.geo.m = v[50]; h.geo.mr = v[51]; h.geo.I0 = v[52]; h.geo.I1 = v[53]; h.geo.kc0 = v[54];
+    h.geo.kc1 = v[55]; h.geo.ra0 = v[56]; h.geo.ra1 = v[57]; h.geo.dimx = v[58]; h.geo.dimy = v[59];
+    h.geo.speed = v[60]; h.geo.rx = v[61];
+    const int fl = (int)v[62];
+    h.phase = fl & 3; h.g32 = (fl & 4) != 0; h.pv32 = (fl & 8) != 0; h.c32 = (fl & 16) != 0;
+    cycle_bounds(h);
 }
 
 /* Robot / Nozzle / SalpRobotEnv constructors (src/robot.py:20-47, 261-412) */

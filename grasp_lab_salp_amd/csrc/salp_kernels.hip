@@ -16,7 +16,7 @@
 using salp::Hot;
 using salp::Params;
 
-#define SF(f) S[(size_t)(f) * (size_t)P.n + (size_t)i]
+#define SF(f) salp::sref(S, P, i, (f))
 
 namespace {
 
@@ -154,7 +154,8 @@ __global__ __launch_bounds__(kBlock) void k_step_random(double* S, Params P, int
 // per env-step.  Per-env results depend only on (seed, env id): how the work
 // is cut into launches and chunks changes nothing but the count of env-steps
 // a launch completes.
-__device__ __forceinline__ void rollout_boundary(Hot& h, double* S, const Params& P, int64_t i,
+template <class ST>
+__device__ __forceinline__ void rollout_boundary(Hot& h, ST S, const Params& P, int64_t i,
                                                  uint64_t env_id, bool& pending, bool& active,
                                                  int64_t& steps, int64_t max_steps,
                                                  const SalpRolloutBuffers& B, salp::Cache32 c32) {
@@ -218,6 +219,11 @@ __device__ __forceinline__ RolloutArgs fresh_args() {
     return a;
 }
 
+// Env-step boundaries park the whole wave's tick state in LDS (SpillSlot),
+// not in HBM: the lanes that need a boundary load their cold fields into
+// registers in one round of loads, run the epilogue/prologue there, store them
+// back, and everyone reloads its tick state from LDS.  HBM sees each env's
+// state once per launch plus the cold rows of the env-steps that end.
 __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
     double* const S = A.S;
     const Params& P = A.P;
@@ -227,6 +233,8 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
     int64_t steps = A.B.steps_done ? A.B.steps_done[i] : 0;
     bool active = !(A.max_steps > 0 && steps >= A.max_steps);
     LANE_CACHE32();
+    __shared__ double s_spill[salp::SPILL_N * salp::LANES];
+    const salp::SpillSlot sp{s_spill + threadIdx.x};
     Hot h;
     salp::load_hot(h, S, P, i);
     salp::resume_cycle(h, S, P, i);
@@ -234,26 +242,27 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
     if (!active) h.b2 = -INFINITY;
     for (int64_t c = 0; c <= A.n_chunks; ++c) {
         // Env-step boundary, taken by the whole wave when any lane needs it.
-        // The tick state goes through memory around it so that no register
-        // holds tick state while the (much larger) epilogue code runs.
         const bool need = active && (!pending || !(h.ct < h.b2));
         const bool last = c == A.n_chunks;
         if (__any(need) || last) {
-            salp::store_hot(h, S, P, i);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            salp::spill(h, sp);
             if (need) {
                 const RolloutArgs a = fresh_args();
                 const uint64_t env_id = (uint64_t)(a.P.env_offset + i);
                 Hot hb;
-                salp::load_hot(hb, a.S, a.P, i, false);
-                salp::resume_cycle(hb, a.S, a.P, i);
-                rollout_boundary(hb, a.S, a.P, i, env_id, pending, active, steps, a.max_steps, a.B, c32);
-                salp::store_hot(hb, a.S, a.P, i);
+                salp::unspill(hb, sp);
+                salp::ColdRegs C;
+                salp::load_cold(C, a.S, a.P, i);
+                rollout_boundary(hb, &C, a.P, i, env_id, pending, active, steps, a.max_steps, a.B, c32);
+                salp::store_cold(C, a.S, a.P, i);
+                salp::spill(hb, sp);
             }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (last) break;
-            salp::load_hot(h, S, P, i);
-            salp::resume_cycle(h, S, P, i);
+            salp::unspill(h, sp);
+            if (last) {
+                const RolloutArgs a = fresh_args();
+                salp::store_hot(h, a.S, a.P, i);
+                break;
+            }
             if (!active) h.b2 = -INFINITY;   // a finished lane ticks no more
         }
         for (int32_t k = 0; k < A.chunk; ++k)
