@@ -71,6 +71,8 @@ SIGNATURES = {
     "salp_state_ptr": (ctypes.c_int64, [_H]),
     "salp_bench_ticks": (ctypes.c_int, [_H, ctypes.c_int32, _V]),
     "salp_math_selftest": (ctypes.c_int, [_V, _V, ctypes.c_int64, _V, _V]),
+    "salp_gae": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64, _V, _V, _V, _V, _V, ctypes.c_double,
+                                ctypes.c_double, _V, _V, _V]),
 }
 
 

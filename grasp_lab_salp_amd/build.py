@@ -8,7 +8,7 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = os.path.join(HERE, "csrc", "salp_kernels.hip")
+SRCS = [os.path.join(HERE, "csrc", f) for f in ("salp_kernels.hip", "salp_gae.hip")]
 OUT = os.path.join(HERE, "libsalp.so")
 ARCH = os.environ.get("SALP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -21,7 +21,7 @@ FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-f
 
 def deps():
     c = os.path.join(HERE, "csrc")
-    return [SRC] + [os.path.join(c, f) for f in os.listdir(c) if f.endswith(".h")] + [
+    return SRCS + [os.path.join(c, f) for f in os.listdir(c) if f.endswith(".h")] + [
         os.path.join(HERE, "..", "include", "salp.h")]
 
 
@@ -35,7 +35,7 @@ def up_to_date():
 def build(force=False, verbose=False, extra=()):
     if not force and up_to_date():
         return OUT
-    cmd = [HIPCC, *FLAGS, *extra, "-o", OUT + ".tmp", SRC]
+    cmd = [HIPCC, *FLAGS, *extra, "-o", OUT + ".tmp", *SRCS]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -435,6 +435,11 @@ Params derive(const SalpParams& p, int64_t n, uint64_t seed, int64_t offset) {
 
 }  // namespace
 
+extern "C" __attribute__((visibility("hidden"))) int salp_gae_launch(
+    int64_t n_steps, int64_t n_envs, const float* rewards, const float* values, const float* episode_starts,
+    const float* last_values, const float* last_dones, double gamma, double gae_lambda, float* advantages,
+    float* returns, void* stream);
+
 extern "C" {
 
 int salp_abi_version(void) { return SALP_ABI_VERSION; }
@@ -640,5 +645,18 @@ int salp_bench_ticks(SalpEnv* h, int32_t n_ticks, void* stream) {
 }
 
 int64_t salp_state_ptr(SalpEnv* h) { return h ? (int64_t)(intptr_t)h->state : 0; }
+
+int salp_gae(int64_t n_steps, int64_t n_envs, const float* rewards, const float* values,
+             const float* episode_starts, const float* last_values, const float* last_dones, double gamma,
+             double gae_lambda, float* advantages, float* returns, void* stream) {
+    if (n_steps < 0 || n_envs < 0) return fail(nullptr, SALP_EINVAL, "salp_gae: negative size");
+    if (!rewards || !values || !episode_starts || !last_values || !last_dones || !advantages || !returns)
+        return fail(nullptr, SALP_EINVAL, "salp_gae: null buffer");
+    if (n_steps == 0 || n_envs == 0) return SALP_OK;
+    if (salp_gae_launch(n_steps, n_envs, rewards, values, episode_starts, last_values, last_dones, gamma,
+                        gae_lambda, advantages, returns, stream) != 0)
+        return fail(nullptr, SALP_EHIP, std::string("k_gae: ") + hipGetErrorString(hipGetLastError()));
+    return SALP_OK;
+}
 
 }  // extern "C"

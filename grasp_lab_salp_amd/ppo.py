@@ -1,0 +1,266 @@
+"""On-device PPO over the batched simulator (BASELINE.json config 5).
+
+The reference trains with Stable-Baselines3 learners (SAC, src/train_robot.py:
+62-69; RecurrentPPO, src/train_robot_recurrent_ppo.py:85-107) on 4-8 envs
+stepped through Python processes.  Here the envs, the rollout buffer, the GAE
+scan (HIP kernel ``salp_gae``) and the policy all stay in HBM:
+
+* collection: ``n_steps`` lock-step env-steps of every env (``salp_step`` with
+  SB3 auto-reset), actions sampled from a diagonal Gaussian MLP policy and
+  clipped to the action box before the step (SB3 ``collect_rollouts``);
+  truncated-not-terminated episodes get ``gamma * V(terminal_obs)`` added to
+  their reward (SB3's timeout bootstrap);
+* advantages / returns: ``salp_gae`` (bit-identical to SB3's NumPy code,
+  oracle/gae.py);
+* update: SB3 PPO's clipped surrogate + value MSE - entropy, advantage
+  normalisation per minibatch, grad-norm clipping, Adam;
+* multi-GPU: one process per GPU, each with its own env shard; gradients are
+  averaged with one flat all-reduce per minibatch (torch.distributed, ``nccl``
+  = RCCL over xGMI; the MLP's gradients are ~20 KB, so one bucket).
+
+The policy is SB3's ``MlpPolicy`` for PPO (separate 64-64 tanh actor and critic,
+orthogonal init, state-independent log-std).  The reference's RecurrentPPO
+uses an LSTM-256 policy; at 32 768 envs its per-step LSTM state buffer would
+not fit, so config 5 runs the MLP policy.  SB3 itself is not
+installed: its semantics are restated, not pinned by a reference test.
+"""
+import ctypes
+import math
+import time
+
+import torch
+import torch.distributed as dist
+from torch import nn
+
+from . import _lib
+
+__all__ = ["compute_gae", "ActorCritic", "RolloutBuffer", "PPO", "allreduce_gradients"]
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def compute_gae(rewards, values, episode_starts, last_values, dones, gamma=0.99, gae_lambda=0.95,
+                advantages=None, returns=None):
+    """SB3 ``compute_returns_and_advantage`` on the GPU (``salp_gae``).
+    All inputs float32 CUDA tensors, [n_steps, n_envs] / [n_envs]."""
+    T, n = rewards.shape
+    for name, t, shape in (("rewards", rewards, (T, n)), ("values", values, (T, n)),
+                           ("episode_starts", episode_starts, (T, n)), ("last_values", last_values, (n,)),
+                           ("dones", dones, (n,))):
+        if not t.is_cuda or t.dtype != torch.float32 or tuple(t.shape) != shape or not t.is_contiguous():
+            raise ValueError(f"{name} must be a contiguous float32 CUDA tensor of shape {shape}")
+    adv = torch.empty_like(rewards) if advantages is None else advantages
+    ret = torch.empty_like(rewards) if returns is None else returns
+    stream = ctypes.c_void_p(torch.cuda.current_stream(rewards.device).cuda_stream)
+    _lib.check(_lib.load().salp_gae(T, n, _ptr(rewards), _ptr(values), _ptr(episode_starts), _ptr(last_values),
+                                    _ptr(dones), float(gamma), float(gae_lambda), _ptr(adv), _ptr(ret), stream))
+    return adv, ret
+
+
+def _ortho(layer, gain):
+    nn.init.orthogonal_(layer.weight, gain=gain)
+    nn.init.zeros_(layer.bias)
+    return layer
+
+
+class ActorCritic(nn.Module):
+    """SB3 ``ActorCriticPolicy`` with ``net_arch=dict(pi=[64, 64], vf=[64, 64])``,
+    tanh, orthogonal init (sqrt(2) hidden, 0.01 action head, 1 value head) and
+    ``log_std_init=0``."""
+
+    def __init__(self, obs_dim, act_dim, hidden=(64, 64)):
+        super().__init__()
+
+        def mlp():
+            layers, d = [], obs_dim
+            for h in hidden:
+                layers += [_ortho(nn.Linear(d, h), math.sqrt(2)), nn.Tanh()]
+                d = h
+            return nn.Sequential(*layers), d
+
+        self.pi_net, d_pi = mlp()
+        self.vf_net, d_vf = mlp()
+        self.action_net = _ortho(nn.Linear(d_pi, act_dim), 0.01)
+        self.value_net = _ortho(nn.Linear(d_vf, 1), 1.0)
+        self.log_std = nn.Parameter(torch.zeros(act_dim))
+
+    def value(self, obs):
+        return self.value_net(self.vf_net(obs)).squeeze(-1)
+
+    def dist(self, obs):
+        mean = self.action_net(self.pi_net(obs))
+        return torch.distributions.Normal(mean, self.log_std.exp().expand_as(mean))
+
+    @torch.no_grad()
+    def act(self, obs):
+        d = self.dist(obs)
+        a = d.sample()
+        return a, self.value(obs), d.log_prob(a).sum(-1)
+
+    def evaluate(self, obs, actions):
+        d = self.dist(obs)
+        return self.value(obs), d.log_prob(actions).sum(-1), d.entropy().sum(-1)
+
+
+class RolloutBuffer:
+    """Device rollout buffer, SB3 layout [n_steps, n_envs, ...] float32."""
+
+    def __init__(self, n_steps, n_envs, obs_dim, act_dim, device):
+        z = lambda *s: torch.zeros(s, dtype=torch.float32, device=device)  # noqa: E731
+        self.obs = z(n_steps, n_envs, obs_dim)
+        self.actions = z(n_steps, n_envs, act_dim)
+        self.rewards = z(n_steps, n_envs)
+        self.episode_starts = z(n_steps, n_envs)
+        self.values = z(n_steps, n_envs)
+        self.log_probs = z(n_steps, n_envs)
+        self.advantages = z(n_steps, n_envs)
+        self.returns = z(n_steps, n_envs)
+        self.n_steps, self.n_envs = n_steps, n_envs
+
+
+def allreduce_gradients(params, group=None):
+    """Average gradients over all ranks with ONE flat all-reduce (a single
+    bucket: the policy is small, so the all-reduce is latency-bound and one
+    message is the cheapest shape for the ring).  No-op without a group."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    world = dist.get_world_size(group)
+    if world == 1:
+        return
+    grads = [p.grad for p in params if p.grad is not None]
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    dist.all_reduce(flat, group=group)
+    flat /= world
+    off = 0
+    for g in grads:
+        k = g.numel()
+        g.copy_(flat[off:off + k].view_as(g))
+        off += k
+
+
+class PPO:
+    """SB3-style PPO on a :class:`~grasp_lab_salp_amd.vec_env.SalpVecEnv`
+    (or anything exposing ``.sim`` = :class:`BatchedSalpEnv`).  Constructor
+    arguments and defaults follow SB3's ``PPO`` (and the reference's
+    RecurrentPPO values where it sets them)."""
+
+    def __init__(self, policy, env, learning_rate=3e-4, n_steps=2048, batch_size=64, n_epochs=10, gamma=0.99,
+                 gae_lambda=0.95, clip_range=0.2, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5,
+                 normalize_advantage=True, seed=0, device=None, verbose=0):
+        if policy not in ("MlpPolicy", None) and not isinstance(policy, nn.Module):
+            raise ValueError("policy must be 'MlpPolicy' or an nn.Module")
+        self.env = env
+        self.sim = getattr(env, "sim", env)
+        self.device = self.sim.device if device is None else torch.device(device)
+        self.n_envs = self.sim.n_envs
+        self.obs_dim = self.sim.obs_dim
+        self.act_dim = 3
+        g = torch.Generator(device="cpu").manual_seed(int(seed))
+        torch.manual_seed(int(seed))
+        self.policy = (policy if isinstance(policy, nn.Module) else ActorCritic(self.obs_dim, self.act_dim)).to(
+            self.device)
+        if dist.is_available() and dist.is_initialized():   # identical initial weights on every rank
+            for p in self.policy.parameters():
+                dist.broadcast(p.data, 0)
+        self.opt = torch.optim.Adam(self.policy.parameters(), lr=learning_rate, eps=1e-5)
+        self.n_steps, self.batch_size, self.n_epochs = int(n_steps), int(batch_size), int(n_epochs)
+        self.gamma, self.gae_lambda, self.clip_range = gamma, gae_lambda, clip_range
+        self.ent_coef, self.vf_coef, self.max_grad_norm = ent_coef, vf_coef, max_grad_norm
+        self.normalize_advantage = normalize_advantage
+        self.verbose = verbose
+        self.gen = g
+        self.buf = RolloutBuffer(self.n_steps, self.n_envs, self.obs_dim, self.act_dim, self.device)
+        self.low = torch.tensor([0.0, 0.0, -1.0], device=self.device)
+        self.high = torch.tensor([1.0, 1.0, 1.0], device=self.device)
+        self._obs = None
+        self._episode_starts = torch.ones(self.n_envs, dtype=torch.float32, device=self.device)
+        self.num_timesteps = 0
+        self.logger = {}
+        self.timing = {"collect_s": 0.0, "gae_s": 0.0, "train_s": 0.0}
+
+    # ---------------------------------------------------------- rollout
+    def collect_rollouts(self):
+        b, sim, pol = self.buf, self.sim, self.policy
+        if self._obs is None:
+            self._obs = sim.reset()
+        for t in range(self.n_steps):
+            obs = self._obs
+            a, v, lp = pol.act(obs)
+            r = sim.step(torch.clamp(a, self.low, self.high), auto_reset=True, want_terminal_obs=True)
+            rew = r.reward.float()
+            trunc_only = r.truncated & ~r.terminated
+            if bool(trunc_only.any()):
+                with torch.no_grad():
+                    tv = pol.value(r.terminal_obs)
+                rew = torch.where(trunc_only, rew + self.gamma * tv, rew)
+            b.obs[t].copy_(obs)
+            b.actions[t].copy_(a)
+            b.rewards[t].copy_(rew)
+            b.episode_starts[t].copy_(self._episode_starts)
+            b.values[t].copy_(v)
+            b.log_probs[t].copy_(lp)
+            self._obs = r.obs
+            self._episode_starts = (r.terminated | r.truncated).float()
+        with torch.no_grad():
+            last_values = pol.value(self._obs).contiguous()
+        t0 = time.perf_counter()
+        compute_gae(b.rewards, b.values, b.episode_starts, last_values, self._episode_starts.contiguous(),
+                    self.gamma, self.gae_lambda, b.advantages, b.returns)
+        return t0
+
+    # ----------------------------------------------------------- update
+    def train(self):
+        b, pol = self.buf, self.policy
+        N = self.n_steps * self.n_envs
+        obs = b.obs.reshape(N, -1)
+        act = b.actions.reshape(N, -1)
+        old_lp = b.log_probs.reshape(N)
+        adv_all = b.advantages.reshape(N)
+        ret = b.returns.reshape(N)
+        stats = {"pg_loss": 0.0, "vf_loss": 0.0, "entropy": 0.0, "clip_frac": 0.0, "n": 0}
+        for _ in range(self.n_epochs):
+            perm = torch.randperm(N, generator=self.gen).to(self.device)
+            for s in range(0, N, self.batch_size):
+                idx = perm[s:s + self.batch_size]
+                v, lp, ent = pol.evaluate(obs[idx], act[idx])
+                adv = adv_all[idx]
+                if self.normalize_advantage and len(idx) > 1:
+                    adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+                ratio = torch.exp(lp - old_lp[idx])
+                pg = -torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - self.clip_range, 1 + self.clip_range)).mean()
+                vf = torch.nn.functional.mse_loss(ret[idx], v)
+                ent_loss = -ent.mean()
+                loss = pg + self.ent_coef * ent_loss + self.vf_coef * vf
+                self.opt.zero_grad(set_to_none=False)
+                loss.backward()
+                allreduce_gradients(list(pol.parameters()))
+                nn.utils.clip_grad_norm_(pol.parameters(), self.max_grad_norm)
+                self.opt.step()
+                stats["pg_loss"] += pg.detach()
+                stats["vf_loss"] += vf.detach()
+                stats["entropy"] += -ent_loss.detach()
+                stats["clip_frac"] += ((ratio - 1).abs() > self.clip_range).float().mean().detach()
+                stats["n"] += 1
+        n = max(stats.pop("n"), 1)
+        return {k: float(v) / n for k, v in stats.items()}
+
+    def learn(self, total_timesteps, log_interval=1):
+        it = 0
+        while self.num_timesteps < total_timesteps:
+            t0 = time.perf_counter()
+            tg = self.collect_rollouts()
+            torch.cuda.synchronize(self.device)
+            t1 = time.perf_counter()
+            self.logger = self.train()
+            torch.cuda.synchronize(self.device)
+            t2 = time.perf_counter()
+            self.timing["collect_s"] += tg - t0
+            self.timing["gae_s"] += t1 - tg
+            self.timing["train_s"] += t2 - t1
+            self.num_timesteps += self.n_steps * self.n_envs
+            it += 1
+            if self.verbose and it % log_interval == 0:
+                print({"iteration": it, "timesteps": self.num_timesteps, **self.logger}, flush=True)
+        return self

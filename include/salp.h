@@ -136,6 +136,20 @@ int salp_rollout(SalpEnv* h, int64_t tick_budget, const SalpRolloutBuffers* buf,
  * env-steps (one full cycle each) with auto-reset.  rewards_out [n] = sum. */
 int salp_step_random(SalpEnv* h, int32_t n_steps, double* reward_sum_out, void* stream);
 
+/* GAE / returns over a rollout buffer: stable_baselines3's
+ * RolloutBuffer.compute_returns_and_advantage (stable-baselines3 >= 2.0,
+ * requirements.txt:6-7), which RecurrentPPO runs with gamma 0.99 and
+ * gae_lambda 0.95 (src/train_robot_recurrent_ppo.py:94-95).  All buffers are
+ * float32 device arrays, [n_steps][n_envs] row-major as in SB3:
+ * rewards, values, episode_starts (1.0 where the step began an episode);
+ * last_values / last_dones [n_envs] are the value estimate and done flag after
+ * the last step.  Outputs advantages, returns [n_steps][n_envs].  Float32 with
+ * SB3's operation order and NumPy 2 promotion (float32(gamma),
+ * float32(gamma * gae_lambda)): bit-identical to the NumPy code. */
+int salp_gae(int64_t n_steps, int64_t n_envs, const float* rewards, const float* values,
+             const float* episode_starts, const float* last_values, const float* last_dones,
+             double gamma, double gae_lambda, float* advantages, float* returns, void* stream);
+
 /* ------------------------------------------------ Robot / Nozzle level */
 /* The reference's Robot API for callers that drive the robot directly,
  * without the task env (src/compare_trajectories.py:120-168,

@@ -1,0 +1,94 @@
+"""BASELINE.json config 5: PPO on 32 768 envs per GPU with the HIP GAE scan.
+
+    python tools/bench_ppo.py [--n-envs 32768] [--n-steps 32] [--iters 2]
+    python -m torch.distributed.run --nproc-per-node N tools/bench_ppo.py ...
+
+Prints one JSON line: full-iteration env-steps/s (collection + GAE + update,
+max time over ranks), the split, and the GAE kernel alone against the HBM
+roofline (12 B read + 8 B written per (step, env), HIP events on the stream
+it runs on).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0
+
+
+def gae_roofline(T, n, reps=20):
+    from grasp_lab_salp_amd.ppo import compute_gae
+    g = torch.Generator(device="cuda").manual_seed(0)
+    rew = torch.randn(T, n, device="cuda", generator=g)
+    val = torch.randn(T, n, device="cuda", generator=g)
+    st = (torch.rand(T, n, device="cuda", generator=g) < 0.02).float()
+    lv, dn = torch.randn(n, device="cuda", generator=g), torch.zeros(n, device="cuda")
+    adv, ret = torch.empty_like(rew), torch.empty_like(rew)
+    compute_gae(rew, val, st, lv, dn, advantages=adv, returns=ret)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        compute_gae(rew, val, st, lv, dn, advantages=adv, returns=ret)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    byts = T * n * 20 + n * 8
+    gbs = byts / (ms / 1e3) / 1e9
+    return {"n_steps": T, "n_envs": n, "ms": ms, "bytes": byts,
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs / HBM_PEAK_GBS}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n-envs", type=int, default=32768)
+    ap.add_argument("--n-steps", type=int, default=32)
+    ap.add_argument("--batch-size", type=int, default=32768)
+    ap.add_argument("--n-epochs", type=int, default=10)
+    ap.add_argument("--iters", type=int, default=2)
+    ap.add_argument("--gae-steps", type=int, default=2048)
+    a = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from grasp_lab_salp_amd.ppo import PPO
+    from grasp_lab_salp_amd.shard import env_id_offset, reduce_run
+    from grasp_lab_salp_amd.vec_env import SalpVecEnv
+    env = SalpVecEnv(a.n_envs, seed=0, env_id_offset=env_id_offset(rank, a.n_envs), infos=False)
+    model = PPO("MlpPolicy", env, n_steps=a.n_steps, batch_size=a.batch_size, n_epochs=a.n_epochs, seed=0)
+    model.learn(a.n_steps * a.n_envs)   # warm-up iteration
+    for k in model.timing:
+        model.timing[k] = 0.0
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    model.num_timesteps = 0
+    model.learn(a.iters * a.n_steps * a.n_envs)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    el, steps, _, _ = reduce_run(el, model.num_timesteps, 0.0, 0.0, device=torch.device("cuda", local))
+    if rank == 0:
+        res = {"metric": "PPO env-steps/sec (collect + GAE + update), config 5", "value": steps / el,
+               "unit": "env-steps/s", "n_gpus": world, "n_envs_per_gpu": a.n_envs, "n_steps": a.n_steps,
+               "batch_size": a.batch_size, "n_epochs": a.n_epochs, "iters": a.iters,
+               "timing_s": model.timing, "losses": model.logger,
+               "gae_kernel": gae_roofline(a.gae_steps, a.n_envs)}
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
