@@ -91,7 +91,7 @@ class ActorCritic(nn.Module):
 
     def dist(self, obs):
         mean = self.action_net(self.pi_net(obs))
-        return torch.distributions.Normal(mean, self.log_std.exp().expand_as(mean))
+        return torch.distributions.Normal(mean, self.log_std.exp().expand_as(mean), validate_args=False)
 
     @torch.no_grad()
     def act(self, obs):
@@ -148,7 +148,7 @@ class PPO:
 
     def __init__(self, policy, env, learning_rate=3e-4, n_steps=2048, batch_size=64, n_epochs=10, gamma=0.99,
                  gae_lambda=0.95, clip_range=0.2, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5,
-                 normalize_advantage=True, seed=0, device=None, verbose=0):
+                 normalize_advantage=True, seed=0, device=None, verbose=0, reset_nonfinite=True):
         if policy not in ("MlpPolicy", None) and not isinstance(policy, nn.Module):
             raise ValueError("policy must be 'MlpPolicy' or an nn.Module")
         self.env = env
@@ -170,6 +170,8 @@ class PPO:
         self.ent_coef, self.vf_coef, self.max_grad_norm = ent_coef, vf_coef, max_grad_norm
         self.normalize_advantage = normalize_advantage
         self.verbose = verbose
+        self.reset_nonfinite = reset_nonfinite
+        self.nonfinite_resets = 0
         self.gen = g
         self.buf = RolloutBuffer(self.n_steps, self.n_envs, self.obs_dim, self.act_dim, self.device)
         self.low = torch.tensor([0.0, 0.0, -1.0], device=self.device)
@@ -190,6 +192,8 @@ class PPO:
             a, v, lp = pol.act(obs)
             r = sim.step(torch.clamp(a, self.low, self.high), auto_reset=True, want_terminal_obs=True)
             rew = r.reward.float()
+            if self.reset_nonfinite:
+                self._reset_nonfinite(r, rew)
             trunc_only = r.truncated & ~r.terminated
             if bool(trunc_only.any()):
                 with torch.no_grad():
@@ -209,6 +213,22 @@ class PPO:
         compute_gae(b.rewards, b.values, b.episode_starts, last_values, self._episode_starts.contiguous(),
                     self.gamma, self.gae_lambda, b.advantages, b.returns)
         return t0
+
+    def _reset_nonfinite(self, r, rew):
+        """The reference integrator diverges for some actions (jet_time < dt,
+        tests/test_gpu_parity.py::test_reference_blowup_is_reproduced) and its
+        env then returns NaN observations until the 500-cycle timeout.  A
+        learner cannot consume those: such envs are reset on the spot and the
+        step is recorded as a truncation with reward 0 and no bootstrap."""
+        bad = ~torch.isfinite(r.obs).all(1) | ~torch.isfinite(rew)
+        if not bool(bad.any()):
+            return
+        self.nonfinite_resets += int(bad.sum())
+        fresh = self.sim.reset(mask=bad)
+        r.obs[bad] = fresh[bad]
+        rew[bad] = 0.0
+        r.truncated[bad] = True
+        r.terminated[bad] = True     # terminal: no gamma * V(terminal_obs) bootstrap
 
     # ----------------------------------------------------------- update
     def train(self):
