@@ -10,7 +10,8 @@ import os
 from ._abi import ABI_VERSION, FIELDS, NUM_FIELDS, TRACE_DIM, SalpParams
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsalp.so")
+# SALP_LIB overrides the library path (A/B runs of alternative builds)
+LIB_PATH = os.environ.get("SALP_LIB") or os.path.join(HERE, "libsalp.so")
 
 _lib = None
 
