@@ -6,7 +6,7 @@ drift apart silently.
 """
 import ctypes
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_OBSTACLES = 4
 OBS_DIM_MAX = 6 + 2 * MAX_OBSTACLES
 
@@ -32,6 +32,13 @@ class SalpParams(ctypes.Structure):
         ("height", ctypes.c_int32),
         ("num_obstacles", ctypes.c_int32),
         ("max_cycles", ctypes.c_int32),
+        # randomisation switches (include/salp.h): all off in the reference scripts
+        ("dynamics_randomization", ctypes.c_int32),
+        ("disturbances", ctypes.c_int32),
+        ("action_randomization", ctypes.c_int32),
+        ("observation_randomization", ctypes.c_int32),
+        ("latency", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
     ]
 
     def as_dict(self):
@@ -70,6 +77,9 @@ FIELDS = (
     + ["ep_len", "ep_return", "path_len", "last_px", "last_py", "sum_a0", "sum_a1", "sum_abs_a2",
        "sum_vel", "init_dist"] + [f"sum_r{i}" for i in range(7)]
     + ["act0", "act1", "act2", "pending", "step_count", "episode"]
+    + ["cd", "dfr", "dtr"] + [f"amf{i}" for i in range(3)] + [f"amrf{i}" for i in range(3)]
+    + [f"amt{i}" for i in range(3)] + [f"amrt{i}" for i in range(3)]
+    + [f"ouf{i}" for i in range(3)] + [f"out{i}" for i in range(3)] + ["rng_ctl", "rng_tick"]
 )
 NUM_FIELDS = len(FIELDS)
 FIELD = {name: i for i, name in enumerate(FIELDS)}

@@ -64,6 +64,7 @@ SIGNATURES = {
     "salp_robot_set_control": (ctypes.c_int, [_H, _V, ctypes.c_int, _V]),
     "salp_robot_step_through_cycle": (ctypes.c_int, [_H, _V]),
     "salp_set_trace": (ctypes.c_int, [_H, ctypes.POINTER(SalpTraceBuffer)]),
+    "salp_set_randomization": (ctypes.c_int, [_H] + [ctypes.c_int] * 5),
     "salp_num_fields": (ctypes.c_int, []),
     "salp_field_name": (ctypes.c_char_p, [ctypes.c_int]),
     "salp_trace_dim": (ctypes.c_int, []),

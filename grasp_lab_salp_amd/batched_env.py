@@ -241,6 +241,18 @@ class BatchedSalpEnv:
             raise _lib.SalpError("recording is not enabled (enable_trace)")
         return self._trace
 
+    # --------------------------------------------------- randomisation
+    def set_randomization(self, dynamics=False, disturbances=False, actions=False, observations=False,
+                          latency=False):
+        """The reference's enable_* switches (Robot.enable_dynamic_randomization,
+        enable_disturbances; SalpRobotEnv.enable_action_randomization,
+        enable_observation_randomization, enable_latency) for this batch.  Draws
+        come from the device Philox stream (salp_random.h)."""
+        flags = [int(bool(x)) for x in (dynamics, disturbances, actions, observations, latency)]
+        self._check(_lib.load().salp_set_randomization(self._h, *flags))
+        (self.params.dynamics_randomization, self.params.disturbances, self.params.action_randomization,
+         self.params.observation_randomization, self.params.latency) = flags
+
     # ------------------------------------------------------------ state
     def get_state(self):
         """[NUM_FIELDS, n] fp64 copy of the struct-of-arrays state."""

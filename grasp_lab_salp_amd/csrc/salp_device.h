@@ -31,6 +31,7 @@
 #include "../../include/salp.h"
 #include "salp_math.h"
 #include "salp_philox.h"
+#include "salp_random.h"
 
 #pragma clang fp contract(off)
 
@@ -68,6 +69,8 @@ struct Params {
     double obstacle_radius, x_min, x_max, y_min, y_max, sep;
     double init_angle1, init_angle2;
     int32_t num_obstacles, max_cycles, obs_dim;
+    /* randomisation switches (SalpParams; salp_random.h) */
+    int32_t rand_dyn, rand_dist, rand_act, rand_obs, latency;
     int64_t n;               /* envs on this device (SoA stride) */
     int64_t env_offset;      /* global id of env 0 */
     uint64_t seed;
@@ -330,6 +333,14 @@ struct Hot {
     Geo geo;                                                   /* geometry of (L, W, V, pV) */
     int phase;
     bool g32, pv32, c32;
+    /* randomised kernels only (RAND): this cycle's coefficients, the OU
+     * disturbance states that survive the reference's zeroing (force x, y;
+     * torque z) and the per-env tick counter of the noise stream */
+    struct Rnd {
+        double cd, dfr, dtr, amf0, amf1, amf2, amrf0, amrf1, amrf2, amt0, amt1, amt2;
+        double ouf0, ouf1, out2, tick;
+    } rnd;
+    uint64_t env_id;
 };
 
 /* State access.  The env-step functions below are templates over the state
@@ -354,7 +365,30 @@ SD void refresh_derived(Hot& h, const Params& P) {
     sm_sincos(h.e1, &h.st, &h.cth);
 }
 
+/* the RAND-only part of Hot (set_control / the tick read and write it) */
+SD void load_rnd(Hot& h, const double* S, const Params& P, int64_t i) {
+    Hot::Rnd& r = h.rnd;
+    r.cd = SF(SALP_F_CD); r.dfr = SF(SALP_F_DFR); r.dtr = SF(SALP_F_DTR);
+    r.amf0 = SF(SALP_F_AMF0); r.amf1 = SF(SALP_F_AMF1); r.amf2 = SF(SALP_F_AMF2);
+    r.amrf0 = SF(SALP_F_AMRF0); r.amrf1 = SF(SALP_F_AMRF1); r.amrf2 = SF(SALP_F_AMRF2);
+    r.amt0 = SF(SALP_F_AMT0); r.amt1 = SF(SALP_F_AMT1); r.amt2 = SF(SALP_F_AMT2);
+    r.ouf0 = SF(SALP_F_OUF0); r.ouf1 = SF(SALP_F_OUF1); r.out2 = SF(SALP_F_OUT2);
+    r.tick = SF(SALP_F_RNG_TICK);
+}
+SD void store_rnd(const Hot& h, double* S, const Params& P, int64_t i) {
+    const Hot::Rnd& r = h.rnd;
+    SF(SALP_F_CD) = r.cd; SF(SALP_F_DFR) = r.dfr; SF(SALP_F_DTR) = r.dtr;
+    SF(SALP_F_AMF0) = r.amf0; SF(SALP_F_AMF1) = r.amf1; SF(SALP_F_AMF2) = r.amf2;
+    SF(SALP_F_AMRF0) = r.amrf0; SF(SALP_F_AMRF1) = r.amrf1; SF(SALP_F_AMRF2) = r.amrf2;
+    SF(SALP_F_AMT0) = r.amt0; SF(SALP_F_AMT1) = r.amt1; SF(SALP_F_AMT2) = r.amt2;
+    SF(SALP_F_OUF0) = r.ouf0; SF(SALP_F_OUF1) = r.ouf1; SF(SALP_F_OUT2) = r.out2;
+    SF(SALP_F_RNG_TICK) = r.tick;
+}
+
+template <bool RAND = false>
 SD void load_hot(Hot& h, const double* S, const Params& P, int64_t i, bool derived = true) {
+    h.env_id = (uint64_t)(P.env_offset + i);
+    if (RAND) load_rnd(h, S, P, i);
     h.v0 = SF(SALP_F_V0); h.v1 = SF(SALP_F_V1); h.v2 = SF(SALP_F_V2);
     h.w0 = SF(SALP_F_W0); h.w1 = SF(SALP_F_W1); h.w2 = SF(SALP_F_W2);
     h.a0 = SF(SALP_F_ACC0); h.a1 = SF(SALP_F_ACC1); h.a2 = SF(SALP_F_ACC2);
@@ -376,7 +410,9 @@ SD void load_hot(Hot& h, const double* S, const Params& P, int64_t i, bool deriv
     h.c32 = SF(SALP_F_CONTR32) != 0.0;
     if (derived) refresh_derived(h, P);
 }
+template <bool RAND = false>
 SD void store_hot(const Hot& h, double* S, const Params& P, int64_t i) {
+    if (RAND) store_rnd(h, S, P, i);
     SF(SALP_F_V0) = h.v0; SF(SALP_F_V1) = h.v1; SF(SALP_F_V2) = h.v2;
     SF(SALP_F_W0) = h.w0; SF(SALP_F_W1) = h.w1; SF(SALP_F_W2) = h.w2;
     SF(SALP_F_ACC0) = h.a0; SF(SALP_F_ACC1) = h.a1; SF(SALP_F_ACC2) = h.a2;
@@ -431,7 +467,7 @@ SD void cycle_bounds(Hot& h) {
 /* Recording (REC): rec points at this env's column of a trace sample,
  * rec[col * rs] (include/salp.h SalpTraceBuffer); the force columns are
  * written here, the state columns by record_state after the tick. */
-template <bool REC = false>
+template <bool REC = false, bool RAND = false>
 SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_t rs = 0) {
     /* this cycle's float32-mode geometry, used at the end if the lane is in
      * that mode (issued first so that the LDS latency hides under the tick) */
@@ -439,6 +475,28 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     for (int k = 0; k < C32_N; ++k) k32[k] = c32[k];
     const Geo& g = h.geo;
     const double m = g.m;
+    /* coefficients of this cycle: the reference's means, or (RAND) the
+     * Robot._randomize_parameters draw of set_control */
+    const double cd = RAND ? h.rnd.cd : CD, dfr = RAND ? h.rnd.dfr : DRAG_FORCE_RATIO,
+                 dtr = RAND ? h.rnd.dtr : DRAG_TORQUE_RATIO;
+    const double cam0 = RAND ? h.rnd.amf0 : AMF0, cam1 = RAND ? h.rnd.amf1 : AMF1,
+                 cam2 = RAND ? h.rnd.amf2 : AMF2;
+    const double car0 = RAND ? h.rnd.amrf0 : AMRF, car1 = RAND ? h.rnd.amrf1 : AMRF,
+                 car2 = RAND ? h.rnd.amrf2 : AMRF;
+    const double cat0 = RAND ? h.rnd.amt0 : AMT0, cat1 = RAND ? h.rnd.amt1 : AMT1,
+                 cat2 = RAND ? h.rnd.amt2 : AMT2;
+    /* OUDisturbance.sample (src/robot.py:233-242) of the force (x, y kept) and
+     * torque (z kept) processes, src/robot.py:796-800, 834-838 */
+    double nf0 = 0.0, nf1 = 0.0, nt2 = 0.0;
+    if (RAND && P.rand_dist) {
+        double z0, z1, z2;
+        sr_normals3(P.seed, h.env_id, (uint64_t)h.rnd.tick, &z0, &z1, &z2);
+        h.rnd.tick += 1.0;
+        h.rnd.ouf0 = sr_ou_step(h.rnd.ouf0, SR_OU_FORCE_THETA, SR_OU_FORCE_SIGMA, z0);
+        h.rnd.ouf1 = sr_ou_step(h.rnd.ouf1, SR_OU_FORCE_THETA, SR_OU_FORCE_SIGMA, z1);
+        h.rnd.out2 = sr_ou_step(h.rnd.out2, SR_OU_TORQUE_THETA, SR_OU_TORQUE_SIGMA, z2);
+        nf0 = h.rnd.ouf0; nf1 = h.rnd.ouf1; nt2 = h.rnd.out2;
+    }
     /* ---------------- Newton ---------------- */
     /* Coriolis force -w x (M v)  (src/dynamics.py:159-162) */
     double mv0 = m * h.v0, mv1 = m * h.v1, mv2 = m * h.v2;
@@ -446,20 +504,21 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
            cf2 = -(h.w0 * mv1 - h.w1 * mv0);
     /* drag force (src/dynamics.py:110-116) */
     double vn = np_norm3(h.v0, h.v1, h.v2);
-    double df0 = g.kc0 * vn * h.v0 + g.kc0 * h.v0 * DRAG_FORCE_RATIO;
-    double df1 = g.kc1 * vn * h.v1 + g.kc1 * h.v1 * DRAG_FORCE_RATIO;
-    double df2 = g.kc1 * vn * h.v2 + g.kc1 * h.v2 * DRAG_FORCE_RATIO;
+    double df0 = g.kc0 * vn * h.v0 + g.kc0 * h.v0 * dfr;
+    double df1 = g.kc1 * vn * h.v1 + g.kc1 * h.v1 * dfr;
+    double df2 = g.kc1 * vn * h.v2 + g.kc1 * h.v2 * dfr;
     /* jet force, JET phase only (src/robot.py:937-951, src/dynamics.py:87-101) */
     const bool jet = h.phase == JET;
-    double jf0 = jet ? g.mr * (h.d0 * g.speed) * -CD : 0.0;
-    double jf1 = jet ? g.mr * (h.d1 * g.speed) * -CD : 0.0;
-    double jf2 = jet ? g.mr * (h.d2 * g.speed) * -CD : 0.0;
+    double jf0 = jet ? g.mr * (h.d0 * g.speed) * -cd : 0.0;
+    double jf1 = jet ? g.mr * (h.d1 * g.speed) * -cd : 0.0;
+    double jf2 = jet ? g.mr * (h.d2 * g.speed) * -cd : 0.0;
     /* added-mass force (src/dynamics.py:131-141) */
-    double am0 = m * AMF0, am1 = m * AMF1, am2 = m * AMF2, amr = g.mr * AMRF;
+    double am0 = m * cam0, am1 = m * cam1, am2 = m * cam2;
+    double amr0 = g.mr * car0, amr1 = g.mr * car1, amr2 = g.mr * car2;
     double amv0 = am0 * h.v0, amv1 = am1 * h.v1, amv2 = am2 * h.v2;
-    double af0 = -((am0 * h.a0 + (h.w1 * amv2 - h.w2 * amv1)) + amr * h.v0);
-    double af1 = -((am1 * h.a1 + (h.w2 * amv0 - h.w0 * amv2)) + amr * h.v1);
-    double af2 = -((am2 * h.a2 + (h.w0 * amv1 - h.w1 * amv0)) + amr * h.v2);
+    double af0 = -((am0 * h.a0 + (h.w1 * amv2 - h.w2 * amv1)) + amr0 * h.v0);
+    double af1 = -((am1 * h.a1 + (h.w2 * amv0 - h.w0 * amv2)) + amr1 * h.v1);
+    double af2 = -((am2 * h.a2 + (h.w0 * amv1 - h.w1 * amv0)) + amr2 * h.v2);
     /* fictitious forces of the moving center of mass (src/robot.py:806-810);
      * com = (cx, 0, 0) */
     const double cx = h.com, crx = h.comr;
@@ -468,9 +527,16 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     double acc_x = (h.w1 * -(h.w1 * cx) - h.w2 * (h.w2 * cx)) + h.coma;
     double ff0 = acc_x * m, ff1 = acc_y * m, ff2 = acc_z * m;
     /* total force and linear acceleration (src/dynamics.py:5-10) */
-    double na0 = ((((jf0 + df0) + af0) + cf0) + ff0) / m;
-    double na1 = ((((jf1 + df1) + af1) + cf1) + ff1) / m;
-    double na2 = ((((jf2 + df2) + af2) + cf2) + ff2) / m;
+    double na0, na1, na2;
+    if (RAND) {   /* + force noise (z: zero) */
+        na0 = (((((jf0 + df0) + af0) + cf0) + nf0) + ff0) / m;
+        na1 = (((((jf1 + df1) + af1) + cf1) + nf1) + ff1) / m;
+        na2 = (((((jf2 + df2) + af2) + cf2) + 0.0) + ff2) / m;
+    } else {
+        na0 = ((((jf0 + df0) + af0) + cf0) + ff0) / m;
+        na1 = ((((jf1 + df1) + af1) + cf1) + ff1) / m;
+        na2 = ((((jf2 + df2) + af2) + cf2) + ff2) / m;
+    }
     /* ---------------- Euler ---------------- */
     const double I0 = g.I0, I1 = g.I1;
     /* Coriolis torque -w x (I w) (src/dynamics.py:165-168) */
@@ -479,9 +545,9 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
            ct2 = -(h.w0 * iw1 - h.w1 * iw0);
     /* drag torque (src/dynamics.py:119-128) */
     double wn = np_norm3(h.w0, h.w1, h.w2);
-    double dt0 = g.ra0 * wn * h.w0 * g.dimx + g.ra0 * h.w0 * h.W * DRAG_TORQUE_RATIO;
-    double dt1 = g.ra1 * wn * h.w1 * g.dimy + g.ra1 * h.w1 * h.W * DRAG_TORQUE_RATIO;
-    double dt2 = g.ra1 * wn * h.w2 * g.dimy + g.ra1 * h.w2 * h.W * DRAG_TORQUE_RATIO;
+    double dt0 = g.ra0 * wn * h.w0 * g.dimx + g.ra0 * h.w0 * h.W * dtr;
+    double dt1 = g.ra1 * wn * h.w1 * g.dimy + g.ra1 * h.w1 * h.W * dtr;
+    double dt2 = g.ra1 * wn * h.w2 * g.dimy + g.ra1 * h.w2 * h.W * dtr;
     /* jet torque r x F, r = (mid_x - L/2, 0, 0) (src/robot.py:931-935) */
     double jt1 = -(g.rx * jf2), jt2 = g.rx * jf1;
     /* deformation torque -(dI/dt) w; prev_I <- I (src/robot.py:888-896) */
@@ -491,15 +557,22 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     double dft0 = -(ir0 * h.w0), dft1 = -(ir1 * h.w1), dft2 = -(ir2 * h.w2);
     h.pI0 = I0; h.pI1 = I1; h.pI2 = I1;
     /* added-mass torque, I_rate term identically zero (src/dynamics.py:144-156) */
-    double at0 = I0 * AMT0, at1 = I1 * AMT1, at2 = I1 * AMT2;
+    double at0 = I0 * cat0, at1 = I1 * cat1, at2 = I1 * cat2;
     double atw0 = at0 * h.w0, atw1 = at1 * h.w1, atw2 = at2 * h.w2;
     double amt0 = -((at0 * h.al0 + (h.w1 * atw2 - h.w2 * atw1)) + (h.v1 * amv2 - h.v2 * amv1));
     double amt1 = -((at1 * h.al1 + (h.w2 * atw0 - h.w0 * atw2)) + (h.v2 * amv0 - h.v0 * amv2));
     double amt2 = -((at2 * h.al2 + (h.w0 * atw1 - h.w1 * atw0)) + (h.v0 * amv1 - h.v1 * amv0));
     /* total torque and angular acceleration (src/dynamics.py:13-17) */
-    double nal0 = (((dt0 + ct0) + dft0) + amt0) / I0;
-    double nal1 = ((((jt1 + dt1) + ct1) + dft1) + amt1) / I1;
-    double nal2 = ((((jt2 + dt2) + ct2) + dft2) + amt2) / I1;
+    double nal0, nal1, nal2;
+    if (RAND) {   /* + torque noise (x, y: zero) */
+        nal0 = ((((dt0 + ct0) + dft0) + amt0) + 0.0) / I0;
+        nal1 = (((((jt1 + dt1) + ct1) + dft1) + amt1) + 0.0) / I1;
+        nal2 = (((((jt2 + dt2) + ct2) + dft2) + amt2) + nt2) / I1;
+    } else {
+        nal0 = (((dt0 + ct0) + dft0) + amt0) / I0;
+        nal1 = ((((jt1 + dt1) + ct1) + dft1) + amt1) / I1;
+        nal2 = ((((jt2 + dt2) + ct2) + dft2) + amt2) / I1;
+    }
     if (REC) {
         const double z = 0.0;
         auto put = [&](int col, double x) { rec[(int64_t)col * rs] = x; };
@@ -634,9 +707,33 @@ SD double nozzle_set_angles(ST S, const Params& P, int64_t i, double a1, double 
 
 /* Robot.set_control (src/robot.py:544-592, geometry.py:14-26); c32: the
  * contraction is an np.float32 (contraction**2 is then float32). */
-template <class ST>
+/* this cycle's coefficients: Robot._randomize_parameters (src/robot.py:
+ * 594-628) when dynamics randomisation is on, else the means (:553-561) */
+template <bool RAND, class ST>
+SD void set_coefficients(Hot& h, ST S, const Params& P, int64_t i) {
+    SrCoef k;
+    if (RAND && P.rand_dyn) {
+        sr_draw_coefs(P.seed, h.env_id, (uint64_t)SF(SALP_F_RNG_CTL), &k);
+        SF(SALP_F_RNG_CTL) = SF(SALP_F_RNG_CTL) + 1.0;
+    } else {
+        sr_coef_means(&k);
+    }
+    SF(SALP_F_CD) = k.cd; SF(SALP_F_DFR) = k.dfr; SF(SALP_F_DTR) = k.dtr;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        SF(SALP_F_AMF0 + j) = k.amf[j]; SF(SALP_F_AMRF0 + j) = k.amrf[j];
+        SF(SALP_F_AMT0 + j) = k.amt[j]; SF(SALP_F_AMRT0 + j) = k.amrt[j];
+    }
+    h.rnd.cd = k.cd; h.rnd.dfr = k.dfr; h.rnd.dtr = k.dtr;
+    h.rnd.amf0 = k.amf[0]; h.rnd.amf1 = k.amf[1]; h.rnd.amf2 = k.amf[2];
+    h.rnd.amrf0 = k.amrf[0]; h.rnd.amrf1 = k.amrf[1]; h.rnd.amrf2 = k.amrf[2];
+    h.rnd.amt0 = k.amt[0]; h.rnd.amt1 = k.amt[1]; h.rnd.amt2 = k.amt[2];
+}
+
+template <bool RAND = false, class ST>
 SD void set_control(Hot& h, ST S, const Params& P, int64_t i, double contraction, double coast,
                     double a1, double a2, bool c32) {
+    set_coefficients<RAND>(h, S, P, i);
     SF(SALP_F_AVGV0) = 0.0; SF(SALP_F_AVGV1) = 0.0; SF(SALP_F_AVGV2) = 0.0;
     SF(SALP_F_AVGW0) = 0.0; SF(SALP_F_AVGW1) = 0.0; SF(SALP_F_AVGW2) = 0.0;
     h.c = contraction;
@@ -673,14 +770,24 @@ SD void cycle_prologue(const Hot& h, ST S, const Params& P, int64_t i) {
 /* ------------------------------------------------ env-step prologue */
 /* SalpRobotEnv.step up to step_through_cycle's loop (src/salp_robot_env.py:
  * 196-210): float32 action rescale, IK, set_control, cycle prologue. */
-template <class ST>
+template <bool RAND = false, class ST>
 SD void begin_step(Hot& h, ST S, const Params& P, int64_t i, float a0, float a1, float a2,
                    Cache32 c32) {
     SF(SALP_F_ACT0) = a0; SF(SALP_F_ACT1) = a1; SF(SALP_F_ACT2) = a2;
     /* _rescale_action in float32 (src/salp_robot_env.py:166-174) */
     float r0 = a0 * 0.06f, r1 = a1 * 10.0f, r2 = a2 * (float)(PI / 2);
-    nozzle_solve(S, P, i, (double)r2, true);
-    set_control(h, S, P, i, (double)r0, (double)r1, SF(SALP_F_ANGLE1), SF(SALP_F_ANGLE2), true);
+    if (RAND && P.rand_act) {
+        /* _randomize_actions (:176-181): Python floats from here on, so the
+         * IK and the body geometry run in float64 */
+        const float rr[3] = {r0, r1, r2};
+        double ra[3];
+        sr_randomize_action(P.seed, h.env_id, (uint64_t)SF(SALP_F_STEP_COUNT), rr, ra);
+        nozzle_solve(S, P, i, ra[2], false);
+        set_control<RAND>(h, S, P, i, ra[0], ra[1], SF(SALP_F_ANGLE1), SF(SALP_F_ANGLE2), false);
+    } else {
+        nozzle_solve(S, P, i, (double)r2, true);
+        set_control<RAND>(h, S, P, i, (double)r0, (double)r1, SF(SALP_F_ANGLE1), SF(SALP_F_ANGLE2), true);
+    }
     fill_cache32(P, h.c, c32);
     cycle_prologue(h, S, P, i);
 }
@@ -766,8 +873,8 @@ struct StepOut {
 /* ------------------------------------------------ env-step epilogue */
 /* SalpRobotEnv.step after the cycle (src/salp_robot_env.py:237-299), reward
  * (:349-397), collision (:561-568), episode metrics (:399-447). */
-template <class ST>
-SD StepOut finish_step(const Hot& h, ST S, const Params& P, int64_t i, float* obs,
+template <bool RAND = false, class ST>
+SD StepOut finish_step(Hot& h, ST S, const Params& P, int64_t i, float* obs,
                        double* info) {
     StepOut out;
     const Rot R = rot_zyx(h.e0, h.e1, h.e2);
@@ -817,6 +924,8 @@ SD StepOut finish_step(const Hot& h, ST S, const Params& P, int64_t i, float* ob
     }
     double reward = comp[0] + comp[1] + comp[2] + comp[3] + comp[4] + comp[5] + comp[6];
     observation(h, R, S, P, i, obs);
+    /* _randomize_observations (src/salp_robot_env.py:183-194, 253-254) */
+    if (RAND && P.rand_obs) sr_randomize_obs(P.seed, h.env_id, (uint64_t)SF(SALP_F_STEP_COUNT), obs);
     /* _check_obstacle_collision with get_current_length() */
     bool l32;
     double Lc, Wc;
@@ -873,6 +982,12 @@ SD StepOut finish_step(const Hot& h, ST S, const Params& P, int64_t i, float* ob
     }
     SF(SALP_F_PREV_A2) = (double)a2;
     SF(SALP_F_PENDING) = 0.0;
+    if (RAND && P.latency) {
+        /* latency (src/salp_robot_env.py:292-297): set_control(contraction=0,
+         * coast_time=U(0, 0.1), current nozzle angles) without a cycle */
+        const double lat = sr_latency(P.seed, h.env_id, (uint64_t)SF(SALP_F_STEP_COUNT));
+        set_control<RAND>(h, S, P, i, 0.0, lat, SF(SALP_F_ANGLE1), SF(SALP_F_ANGLE2), false);
+    }
     out.reward = reward;
     out.terminated = done;
     out.truncated = trunc;
@@ -941,6 +1056,10 @@ SD void robot_reset(Hot& h, ST S, const Params& P, int64_t i) {
     h.pV = h.V; h.pv32 = false;
     refresh_derived(h, P);
     h.pI0 = h.geo.I0; h.pI1 = h.geo.I1; h.pI2 = h.geo.I1;
+    /* force_disturbance.reset(), torque_disturbance.reset() (src/robot.py:454-455) */
+    SF(SALP_F_OUF0) = 0.0; SF(SALP_F_OUF1) = 0.0; SF(SALP_F_OUF2) = 0.0;
+    SF(SALP_F_OUT0) = 0.0; SF(SALP_F_OUT1) = 0.0; SF(SALP_F_OUT2) = 0.0;
+    h.rnd.ouf0 = 0.0; h.rnd.ouf1 = 0.0; h.rnd.out2 = 0.0;
     SF(SALP_F_PENDING) = 0.0;
 }
 
@@ -987,44 +1106,61 @@ SD void reset_env_philox(Hot& h, ST S, const Params& P, int64_t i, float* obs) {
 
 /* ------------------------------------- rollout boundary: LDS + registers */
 /* Fields store_hot writes (the tick's state); every other field is "cold":
- * touched only at env-step boundaries. */
+ * touched only at env-step boundaries.  RAND kernels also carry Hot::Rnd. */
+SD constexpr bool is_rnd(int f) {
+    return (f >= SALP_F_CD && f <= SALP_F_DTR) || (f >= SALP_F_AMF0 && f <= SALP_F_AMRF2) ||
+           (f >= SALP_F_AMT0 && f <= SALP_F_AMT2) || f == SALP_F_OUF0 || f == SALP_F_OUF1 ||
+           f == SALP_F_OUT2 || f == SALP_F_RNG_TICK;
+}
+template <bool RAND>
 SD constexpr bool is_hot(int f) {
     return (f >= SALP_F_V0 && f <= SALP_F_ANG2) || (f >= SALP_F_LENGTH && f <= SALP_F_PVOL32) ||
-           (f >= SALP_F_CYCLE_TIME && f <= SALP_F_PHASE) || f == SALP_F_CONTR32 || f == SALP_F_TURN_TIME;
+           (f >= SALP_F_CYCLE_TIME && f <= SALP_F_PHASE) || f == SALP_F_CONTR32 || f == SALP_F_TURN_TIME ||
+           (RAND && is_rnd(f));
 }
 /* One env's cold fields into registers with all loads in flight at once. */
+template <bool RAND>
 SD void load_cold(ColdRegs& C, const double* S, const Params& P, int64_t i) {
 #pragma unroll
     for (int f = 0; f < SALP_NUM_FIELDS; ++f)
-        if (!is_hot(f)) C.v[f] = S[(size_t)f * (size_t)P.n + (size_t)i];
+        if (!is_hot<RAND>(f)) C.v[f] = S[(size_t)f * (size_t)P.n + (size_t)i];
 }
+template <bool RAND>
 SD void store_cold(const ColdRegs& C, double* S, const Params& P, int64_t i) {
 #pragma unroll
     for (int f = 0; f < SALP_NUM_FIELDS; ++f)
-        if (!is_hot(f)) S[(size_t)f * (size_t)P.n + (size_t)i] = C.v[f];
+        if (!is_hot<RAND>(f)) S[(size_t)f * (size_t)P.n + (size_t)i] = C.v[f];
 }
 
 /* A lane's slot of a workgroup LDS array [SPILL_N][LANES]: the whole Hot
- * state (geometry and roll/pitch sin/cos included, so nothing is recomputed
- * on reload) parks here while the wave runs an env-step boundary. */
+ * state parks here while the wave runs an env-step boundary.  Plain kernels
+ * park the geometry and roll/pitch sin/cos too (nothing recomputed on
+ * reload); RAND kernels park Hot::Rnd in those slots instead and recompute
+ * the geometry on reload. */
 constexpr int SPILL_N = 63;
 struct SpillSlot {
     double* p;
     SD_MEMBER double& operator[](int k) const { return p[k * LANES]; }
 };
+template <bool RAND>
 SD void spill(const Hot& h, SpillSlot s) {
+    const Hot::Rnd& r = h.rnd;
     const double v[SPILL_N] = {
         h.v0, h.v1, h.v2, h.w0, h.w1, h.w2, h.a0, h.a1, h.a2, h.al0, h.al1, h.al2,
         h.e0, h.e1, h.e2, h.p0, h.p1, h.p2, h.q0, h.q1, h.q2, h.g0, h.g1, h.g2,
         h.L, h.W, h.V, h.pV, h.com, h.comr, h.coma, h.pI0, h.pI1, h.pI2, h.ct, h.time,
-        h.refill, h.jet, h.coast, h.c, h.cr, h.rr, h.turn, h.d0, h.d1, h.d2, h.sp, h.cp, h.st, h.cth,
-        h.geo.m, h.geo.mr, h.geo.I0, h.geo.I1, h.geo.kc0, h.geo.kc1, h.geo.ra0, h.geo.ra1,
-        h.geo.dimx, h.geo.dimy, h.geo.speed, h.geo.rx,
-        (double)(h.phase | (h.g32 ? 4 : 0) | (h.pv32 ? 8 : 0) | (h.c32 ? 16 : 0))};
+        h.refill, h.jet, h.coast, h.c, h.cr, h.rr, h.turn, h.d0, h.d1, h.d2,
+        (double)(h.phase | (h.g32 ? 4 : 0) | (h.pv32 ? 8 : 0) | (h.c32 ? 16 : 0)),
+        RAND ? r.cd : h.sp, RAND ? r.dfr : h.cp, RAND ? r.dtr : h.st, RAND ? r.amf0 : h.cth,
+        RAND ? r.amf1 : h.geo.m, RAND ? r.amf2 : h.geo.mr, RAND ? r.amrf0 : h.geo.I0,
+        RAND ? r.amrf1 : h.geo.I1, RAND ? r.amrf2 : h.geo.kc0, RAND ? r.amt0 : h.geo.kc1,
+        RAND ? r.amt1 : h.geo.ra0, RAND ? r.amt2 : h.geo.ra1, RAND ? r.ouf0 : h.geo.dimx,
+        RAND ? r.ouf1 : h.geo.dimy, RAND ? r.out2 : h.geo.speed, RAND ? r.tick : h.geo.rx};
 #pragma unroll
     for (int k = 0; k < SPILL_N; ++k) s[k] = v[k];
 }
-SD void unspill(Hot& h, SpillSlot s) {
+template <bool RAND>
+SD void unspill(Hot& h, SpillSlot s, const Params& P, uint64_t env_id) {
     double v[SPILL_N];
 #pragma unroll
     for (int k = 0; k < SPILL_N; ++k) v[k] = s[k];
@@ -1036,12 +1172,21 @@ SD void unspill(Hot& h, SpillSlot s) {
     h.pI0 = v[31]; h.pI1 = v[32]; h.pI2 = v[33]; h.ct = v[34]; h.time = v[35];
     h.refill = v[36]; h.jet = v[37]; h.coast = v[38]; h.c = v[39]; h.cr = v[40]; h.rr = v[41];
     h.turn = v[42]; h.d0 = v[43]; h.d1 = v[44]; h.d2 = v[45];
-    h.sp = v[46]; h.cp = v[47]; h.st = v[48]; h.cth = v[49];
-    h.geo.m = v[50]; h.geo.mr = v[51]; h.geo.I0 = v[52]; h.geo.I1 = v[53]; h.geo.kc0 = v[54];
-    h.geo.kc1 = v[55]; h.geo.ra0 = v[56]; h.geo.ra1 = v[57]; h.geo.dimx = v[58]; h.geo.dimy = v[59];
-    h.geo.speed = v[60]; h.geo.rx = v[61];
-    const int fl = (int)v[62];
+    const int fl = (int)v[46];
     h.phase = fl & 3; h.g32 = (fl & 4) != 0; h.pv32 = (fl & 8) != 0; h.c32 = (fl & 16) != 0;
+    h.env_id = env_id;
+    if (RAND) {
+        Hot::Rnd& r = h.rnd;
+        r.cd = v[47]; r.dfr = v[48]; r.dtr = v[49]; r.amf0 = v[50]; r.amf1 = v[51]; r.amf2 = v[52];
+        r.amrf0 = v[53]; r.amrf1 = v[54]; r.amrf2 = v[55]; r.amt0 = v[56]; r.amt1 = v[57];
+        r.amt2 = v[58]; r.ouf0 = v[59]; r.ouf1 = v[60]; r.out2 = v[61]; r.tick = v[62];
+        refresh_derived(h, P);
+    } else {
+        h.sp = v[47]; h.cp = v[48]; h.st = v[49]; h.cth = v[50];
+        h.geo.m = v[51]; h.geo.mr = v[52]; h.geo.I0 = v[53]; h.geo.I1 = v[54]; h.geo.kc0 = v[55];
+        h.geo.kc1 = v[56]; h.geo.ra0 = v[57]; h.geo.ra1 = v[58]; h.geo.dimx = v[59]; h.geo.dimy = v[60];
+        h.geo.speed = v[61]; h.geo.rx = v[62];
+    }
     cycle_bounds(h);
 }
 
@@ -1061,6 +1206,13 @@ SD void construct_env(double* S, const Params& P, int64_t i) {
     SF(SALP_F_ANGLE1) = P.init_angle1; SF(SALP_F_ANGLE2) = P.init_angle2;
     SF(SALP_F_TURN_TIME) = fabs(P.init_angle1 - 0.0) / P.angle_speed +
                            fabs(P.init_angle2 - 0.0) / P.angle_speed;
+    SrCoef k;
+    sr_coef_means(&k);
+    SF(SALP_F_CD) = k.cd; SF(SALP_F_DFR) = k.dfr; SF(SALP_F_DTR) = k.dtr;
+    for (int j = 0; j < 3; ++j) {
+        SF(SALP_F_AMF0 + j) = k.amf[j]; SF(SALP_F_AMRF0 + j) = k.amrf[j];
+        SF(SALP_F_AMT0 + j) = k.amt[j]; SF(SALP_F_AMRT0 + j) = k.amrt[j];
+    }
 }
 
 #undef SF

@@ -32,12 +32,14 @@ static_assert(kBlock == salp::LANES, "LDS cache stride is the workgroup size");
     __shared__ double s_cache32[salp::C32_N * salp::LANES];         \
     const salp::Cache32 c32{s_cache32 + threadIdx.x}
 
+template <bool RAND>
 __device__ __forceinline__ void run_cycle(Hot& h, const Params& P, salp::Cache32 c32) {
-    for (int g = 0; h.ct < h.b2 && g < kMaxTicksPerCycle; ++g) salp::tick(h, P, c32);
+    for (int g = 0; h.ct < h.b2 && g < kMaxTicksPerCycle; ++g) salp::tick<false, RAND>(h, P, c32);
 }
 
 // The loop of Robot.step_through_cycle with record=True (src/robot.py:
 // 750-765): sample 0 before the first tick, one sample per tick after it.
+template <bool RAND>
 __device__ void run_cycle_recorded(Hot& h, const double* S, const Params& P, salp::Cache32 c32,
                                    const SalpTraceBuffer& T, int64_t i) {
     const int64_t n = P.n;
@@ -47,10 +49,10 @@ __device__ void run_cycle_recorded(Hot& h, const double* S, const Params& P, sal
         ++t;
         if (t < T.max_samples) {
             double* rec = T.rows + (size_t)t * SALP_TRACE_DIM * (size_t)n + (size_t)i;
-            salp::tick<true>(h, P, c32, rec, n);
+            salp::tick<true, RAND>(h, P, c32, rec, n);
             salp::record_state(h, P, S, i, rec, n, false);
         } else {
-            salp::tick(h, P, c32);
+            salp::tick<false, RAND>(h, P, c32);
         }
     }
     T.n_samples[i] = t + 1;
@@ -92,7 +94,7 @@ __global__ __launch_bounds__(kBlock) void k_reset_to(double* S, Params P, const 
 }
 
 // SalpRobotEnv.step for every env (one breathing cycle each).
-template <bool REC>
+template <bool REC, bool RAND>
 __global__ __launch_bounds__(kBlock) void k_step(double* S, Params P, const float* actions,
                                                  float* obs_out, double* reward_out,
                                                  uint8_t* term_out, uint8_t* trunc_out,
@@ -102,13 +104,14 @@ __global__ __launch_bounds__(kBlock) void k_step(double* S, Params P, const floa
     if (i >= P.n) return;
     LANE_CACHE32();
     Hot h;
-    salp::load_hot(h, S, P, i);
-    salp::begin_step(h, S, P, i, actions[3 * i], actions[3 * i + 1], actions[3 * i + 2], c32);
-    if (REC) run_cycle_recorded(h, S, P, c32, T, i);
-    else run_cycle(h, P, c32);
+    salp::load_hot<RAND>(h, S, P, i);
+    salp::begin_step<RAND>(h, S, P, i, actions[3 * i], actions[3 * i + 1], actions[3 * i + 2], c32);
+    if (REC) run_cycle_recorded<RAND>(h, S, P, c32, T, i);
+    else run_cycle<RAND>(h, P, c32);
     SF(SALP_F_STEP_COUNT) = SF(SALP_F_STEP_COUNT) + 1.0;
     float o[SALP_OBS_DIM_MAX];
-    salp::StepOut r = salp::finish_step(h, S, P, i, o, info_out ? info_out + (size_t)SALP_INFO_DIM * i : nullptr);
+    salp::StepOut r =
+        salp::finish_step<RAND>(h, S, P, i, o, info_out ? info_out + (size_t)SALP_INFO_DIM * i : nullptr);
     if (reward_out) reward_out[i] = r.reward;
     if (term_out) term_out[i] = r.terminated;
     if (trunc_out) trunc_out[i] = r.truncated;
@@ -117,32 +120,33 @@ __global__ __launch_bounds__(kBlock) void k_step(double* S, Params P, const floa
     if (auto_reset && (r.terminated || r.truncated)) salp::reset_env_philox(h, S, P, i, o);
     if (obs_out)
         for (int k = 0; k < P.obs_dim; ++k) obs_out[(size_t)i * P.obs_dim + k] = o[k];
-    salp::store_hot(h, S, P, i);
+    salp::store_hot<RAND>(h, S, P, i);
 }
 
 // Lock-step random-action env steps (every env does exactly n_steps).
+template <bool RAND>
 __global__ __launch_bounds__(kBlock) void k_step_random(double* S, Params P, int32_t n_steps,
                                                         double* reward_sum) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.n) return;
     LANE_CACHE32();
     Hot h;
-    salp::load_hot(h, S, P, i);
+    salp::load_hot<RAND>(h, S, P, i);
     const uint64_t env_id = (uint64_t)(P.env_offset + i);
     double rs = 0.0;
     for (int32_t k = 0; k < n_steps; ++k) {
         float a[3];
         sp_action(P.seed, env_id, (uint64_t)SF(SALP_F_STEP_COUNT), a);
-        salp::begin_step(h, S, P, i, a[0], a[1], a[2], c32);
-        run_cycle(h, P, c32);
+        salp::begin_step<RAND>(h, S, P, i, a[0], a[1], a[2], c32);
+        run_cycle<RAND>(h, P, c32);
         SF(SALP_F_STEP_COUNT) = SF(SALP_F_STEP_COUNT) + 1.0;
         float o[SALP_OBS_DIM_MAX];
-        salp::StepOut r = salp::finish_step(h, S, P, i, o, nullptr);
+        salp::StepOut r = salp::finish_step<RAND>(h, S, P, i, o, nullptr);
         rs += r.reward;
         if (r.terminated || r.truncated) salp::reset_env_philox(h, S, P, i, o);
     }
     if (reward_sum) reward_sum[i] = rs;
-    salp::store_hot(h, S, P, i);
+    salp::store_hot<RAND>(h, S, P, i);
 }
 
 // Chained random-action rollout, filling the rollout buffer.  Work proceeds in
@@ -154,7 +158,7 @@ __global__ __launch_bounds__(kBlock) void k_step_random(double* S, Params P, int
 // per env-step.  Per-env results depend only on (seed, env id): how the work
 // is cut into launches and chunks changes nothing but the count of env-steps
 // a launch completes.
-template <class ST>
+template <bool RAND, class ST>
 __device__ __forceinline__ void rollout_boundary(Hot& h, ST S, const Params& P, int64_t i,
                                                  uint64_t env_id, bool& pending, bool& active,
                                                  int64_t& steps, int64_t max_steps,
@@ -165,7 +169,7 @@ __device__ __forceinline__ void rollout_boundary(Hot& h, ST S, const Params& P, 
         if (fin) {
             SF(SALP_F_STEP_COUNT) = SF(SALP_F_STEP_COUNT) + 1.0;
             float o[SALP_OBS_DIM_MAX];
-            salp::StepOut r = salp::finish_step(h, S, P, i, o, nullptr);
+            salp::StepOut r = salp::finish_step<RAND>(h, S, P, i, o, nullptr);
             if (B.capacity > 0) {
                 const size_t slot = (size_t)(steps % B.capacity);
                 const size_t row = slot * (size_t)P.n + (size_t)i;
@@ -188,7 +192,7 @@ __device__ __forceinline__ void rollout_boundary(Hot& h, ST S, const Params& P, 
         if (beg) {
             float a[3];
             sp_action(P.seed, env_id, (uint64_t)SF(SALP_F_STEP_COUNT), a);
-            salp::begin_step(h, S, P, i, a[0], a[1], a[2], c32);
+            salp::begin_step<RAND>(h, S, P, i, a[0], a[1], a[2], c32);
             pending = true;
         }
         if (!fin && !beg) break;
@@ -224,6 +228,7 @@ __device__ __forceinline__ RolloutArgs fresh_args() {
 // registers in one round of loads, run the epilogue/prologue there, store them
 // back, and everyone reloads its tick state from LDS.  HBM sees each env's
 // state once per launch plus the cold rows of the env-steps that end.
+template <bool RAND>
 __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
     double* const S = A.S;
     const Params& P = A.P;
@@ -236,7 +241,7 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
     __shared__ double s_spill[salp::SPILL_N * salp::LANES];
     const salp::SpillSlot sp{s_spill + threadIdx.x};
     Hot h;
-    salp::load_hot(h, S, P, i);
+    salp::load_hot<RAND>(h, S, P, i);
     salp::resume_cycle(h, S, P, i);
     salp::fill_cache32(P, h.c, c32);
     if (!active) h.b2 = -INFINITY;
@@ -245,28 +250,30 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
         const bool need = active && (!pending || !(h.ct < h.b2));
         const bool last = c == A.n_chunks;
         if (__any(need) || last) {
-            salp::spill(h, sp);
+            salp::spill<RAND>(h, sp);
             if (need) {
                 const RolloutArgs a = fresh_args();
                 const uint64_t env_id = (uint64_t)(a.P.env_offset + i);
                 Hot hb;
-                salp::unspill(hb, sp);
+                salp::unspill<RAND>(hb, sp, a.P, env_id);
                 salp::ColdRegs C;
-                salp::load_cold(C, a.S, a.P, i);
-                rollout_boundary(hb, &C, a.P, i, env_id, pending, active, steps, a.max_steps, a.B, c32);
-                salp::store_cold(C, a.S, a.P, i);
-                salp::spill(hb, sp);
+                salp::load_cold<RAND>(C, a.S, a.P, i);
+                rollout_boundary<RAND>(hb, &C, a.P, i, env_id, pending, active, steps, a.max_steps, a.B, c32);
+                salp::store_cold<RAND>(C, a.S, a.P, i);
+                salp::spill<RAND>(hb, sp);
             }
-            salp::unspill(h, sp);
-            if (last) {
+            {
                 const RolloutArgs a = fresh_args();
-                salp::store_hot(h, a.S, a.P, i);
-                break;
+                salp::unspill<RAND>(h, sp, a.P, (uint64_t)(a.P.env_offset + i));
+                if (last) {
+                    salp::store_hot<RAND>(h, a.S, a.P, i);
+                    break;
+                }
             }
             if (!active) h.b2 = -INFINITY;   // a finished lane ticks no more
         }
         for (int32_t k = 0; k < A.chunk; ++k)
-            if (h.ct < h.b2) salp::tick(h, P, c32);
+            if (h.ct < h.b2) salp::tick<false, RAND>(h, P, c32);
     }
     if (A.B.steps_done) A.B.steps_done[i] = steps;
 }
@@ -294,30 +301,31 @@ __global__ __launch_bounds__(kBlock) void k_nozzle_solve(double* S, Params P, co
     salp::nozzle_solve(S, P, i, yaw[i], yaw32 != 0);
 }
 
+template <bool RAND>
 __global__ __launch_bounds__(kBlock) void k_robot_set_control(double* S, Params P, const double* ctl,
                                                               int c32) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.n) return;
     Hot h;
     salp::load_hot(h, S, P, i, false);
-    salp::set_control(h, S, P, i, ctl[4 * i], ctl[4 * i + 1], ctl[4 * i + 2], ctl[4 * i + 3], c32 != 0);
+    salp::set_control<RAND>(h, S, P, i, ctl[4 * i], ctl[4 * i + 1], ctl[4 * i + 2], ctl[4 * i + 3], c32 != 0);
     salp::store_hot(h, S, P, i);
 }
 
-template <bool REC>
+template <bool REC, bool RAND>
 __global__ __launch_bounds__(kBlock) void k_robot_cycle(double* S, Params P, SalpTraceBuffer T) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.n) return;
     LANE_CACHE32();
     Hot h;
-    salp::load_hot(h, S, P, i);
+    salp::load_hot<RAND>(h, S, P, i);
     salp::resume_cycle(h, S, P, i);
     salp::fill_cache32(P, h.c, c32);
     salp::cycle_prologue(h, S, P, i);
-    if (REC) run_cycle_recorded(h, S, P, c32, T, i);
-    else run_cycle(h, P, c32);
+    if (REC) run_cycle_recorded<RAND>(h, S, P, c32, T, i);
+    else run_cycle<RAND>(h, P, c32);
     SF(SALP_F_PENDING) = 0.0;
-    salp::store_hot(h, S, P, i);
+    salp::store_hot<RAND>(h, S, P, i);
 }
 
 // Diagnostic: n_ticks physics ticks on every lane with no env-step boundaries
@@ -330,7 +338,7 @@ __global__ __launch_bounds__(kBlock) void k_tick_bench(double* S, Params P, int3
     salp::load_hot(h, S, P, i);
     salp::resume_cycle(h, S, P, i);
     salp::fill_cache32(P, h.c, c32);
-    for (int32_t k = 0; k < n_ticks; ++k) salp::tick(h, P, c32);
+    for (int32_t k = 0; k < n_ticks; ++k) salp::tick<false, false>(h, P, c32);
     salp::store_hot(h, S, P, i);
 }
 
@@ -364,7 +372,10 @@ const char* const kFieldNames[SALP_NUM_FIELDS] = {
     "n_obst", "prev_dist", "prev_a2",
     "ep_len", "ep_return", "path_len", "last_px", "last_py", "sum_a0", "sum_a1", "sum_abs_a2",
     "sum_vel", "init_dist", "sum_r0", "sum_r1", "sum_r2", "sum_r3", "sum_r4", "sum_r5", "sum_r6",
-    "act0", "act1", "act2", "pending", "step_count", "episode"};
+    "act0", "act1", "act2", "pending", "step_count", "episode",
+    "cd", "dfr", "dtr", "amf0", "amf1", "amf2", "amrf0", "amrf1", "amrf2",
+    "amt0", "amt1", "amt2", "amrt0", "amrt1", "amrt2",
+    "ouf0", "ouf1", "ouf2", "out0", "out1", "out2", "rng_ctl", "rng_tick"};
 
 thread_local std::string g_last_error;
 
@@ -397,6 +408,9 @@ int launched(SalpEnv* h, const char* what) { return check_hip(h, hipGetLastError
 
 unsigned blocks_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
+// Any randomisation switch on: launch the RAND instantiation of the kernels.
+bool randomized(const Params& d) { return d.rand_dyn || d.rand_dist || d.rand_act || d.rand_obs || d.latency; }
+
 // Launch-invariant constants; the same IEEE expressions as the oracle.
 Params derive(const SalpParams& p, int64_t n, uint64_t seed, int64_t offset) {
     Params d{};
@@ -427,6 +441,11 @@ Params derive(const SalpParams& p, int64_t n, uint64_t seed, int64_t offset) {
     d.num_obstacles = p.num_obstacles;
     d.max_cycles = p.max_cycles;
     d.obs_dim = 6 + 2 * p.num_obstacles;
+    d.rand_dyn = p.dynamics_randomization != 0;
+    d.rand_dist = p.disturbances != 0;
+    d.rand_act = p.action_randomization != 0;
+    d.rand_obs = p.observation_randomization != 0;
+    d.latency = p.latency != 0;
     d.n = n;
     d.env_offset = offset;
     d.seed = seed;
@@ -530,22 +549,19 @@ int salp_step(SalpEnv* h, const float* actions, float* obs_out, double* reward_o
               float* terminal_obs_out, double* info_out, void* stream) {
     if (!h) return fail(nullptr, SALP_EINVAL, "salp_step: null handle");
     if (!actions) return fail(h, SALP_EINVAL, "salp_step: actions is required");
-    if (h->trace.max_samples > 0)
-        hipLaunchKernelGGL(k_step<true>, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream,
-                           h->state, h->dp, actions, obs_out, reward_out, terminated_out, truncated_out,
-                           auto_reset, terminal_obs_out, info_out, h->trace);
-    else
-        hipLaunchKernelGGL(k_step<false>, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream,
-                           h->state, h->dp, actions, obs_out, reward_out, terminated_out, truncated_out,
-                           auto_reset, terminal_obs_out, info_out, h->trace);
+    auto kern = h->trace.max_samples > 0 ? (randomized(h->dp) ? k_step<true, true> : k_step<true, false>)
+                                         : (randomized(h->dp) ? k_step<false, true> : k_step<false, false>);
+    hipLaunchKernelGGL(kern, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream, h->state, h->dp,
+                       actions, obs_out, reward_out, terminated_out, truncated_out, auto_reset, terminal_obs_out,
+                       info_out, h->trace);
     return launched(h, "k_step");
 }
 
 int salp_step_random(SalpEnv* h, int32_t n_steps, double* reward_sum_out, void* stream) {
     if (!h) return fail(nullptr, SALP_EINVAL, "salp_step_random: null handle");
     if (n_steps < 0) return fail(h, SALP_EINVAL, "salp_step_random: n_steps < 0");
-    hipLaunchKernelGGL(k_step_random, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream,
-                       h->state, h->dp, n_steps, reward_sum_out);
+    hipLaunchKernelGGL(randomized(h->dp) ? k_step_random<true> : k_step_random<false>, dim3(blocks_for(h->n)),
+                       dim3(kBlock), 0, (hipStream_t)stream, h->state, h->dp, n_steps, reward_sum_out);
     return launched(h, "k_step_random");
 }
 
@@ -558,7 +574,8 @@ int salp_rollout(SalpEnv* h, int64_t tick_budget, const SalpRolloutBuffers* buf,
     int32_t chunk = b.chunk > 0 ? b.chunk : 128;
     int64_t n_chunks = (tick_budget + chunk - 1) / chunk;
     RolloutArgs args{h->state, h->dp, n_chunks, chunk, b.max_steps, b};
-    hipLaunchKernelGGL(k_rollout, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream, args);
+    hipLaunchKernelGGL(randomized(h->dp) ? k_rollout<true> : k_rollout<false>, dim3(blocks_for(h->n)),
+                       dim3(kBlock), 0, (hipStream_t)stream, args);
     return launched(h, "k_rollout");
 }
 
@@ -588,19 +605,19 @@ int salp_nozzle_solve(SalpEnv* h, const double* yaw, int yaw_is_f32, void* strea
 int salp_robot_set_control(SalpEnv* h, const double* control, int contraction_is_f32, void* stream) {
     if (!h) return fail(nullptr, SALP_EINVAL, "salp_robot_set_control: null handle");
     if (!control) return fail(h, SALP_EINVAL, "salp_robot_set_control: control is required");
-    hipLaunchKernelGGL(k_robot_set_control, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream,
-                       h->state, h->dp, control, contraction_is_f32);
+    hipLaunchKernelGGL(randomized(h->dp) ? k_robot_set_control<true> : k_robot_set_control<false>,
+                       dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream, h->state, h->dp, control,
+                       contraction_is_f32);
     return launched(h, "k_robot_set_control");
 }
 
 int salp_robot_step_through_cycle(SalpEnv* h, void* stream) {
     if (!h) return fail(nullptr, SALP_EINVAL, "salp_robot_step_through_cycle: null handle");
-    if (h->trace.max_samples > 0)
-        hipLaunchKernelGGL(k_robot_cycle<true>, dim3(blocks_for(h->n)), dim3(kBlock), 0,
-                           (hipStream_t)stream, h->state, h->dp, h->trace);
-    else
-        hipLaunchKernelGGL(k_robot_cycle<false>, dim3(blocks_for(h->n)), dim3(kBlock), 0,
-                           (hipStream_t)stream, h->state, h->dp, h->trace);
+    auto kern = h->trace.max_samples > 0
+                    ? (randomized(h->dp) ? k_robot_cycle<true, true> : k_robot_cycle<true, false>)
+                    : (randomized(h->dp) ? k_robot_cycle<false, true> : k_robot_cycle<false, false>);
+    hipLaunchKernelGGL(kern, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream, h->state, h->dp,
+                       h->trace);
     return launched(h, "k_robot_cycle");
 }
 
@@ -613,6 +630,17 @@ int salp_set_trace(SalpEnv* h, const SalpTraceBuffer* buf) {
     if (!buf->rows || !buf->n_samples)
         return fail(h, SALP_EINVAL, "salp_set_trace: rows and n_samples are required");
     h->trace = *buf;
+    return SALP_OK;
+}
+
+int salp_set_randomization(SalpEnv* h, int dynamics, int disturbances, int actions, int observations,
+                           int latency) {
+    if (!h) return fail(nullptr, SALP_EINVAL, "salp_set_randomization: null handle");
+    h->params.dynamics_randomization = h->dp.rand_dyn = dynamics != 0;
+    h->params.disturbances = h->dp.rand_dist = disturbances != 0;
+    h->params.action_randomization = h->dp.rand_act = actions != 0;
+    h->params.observation_randomization = h->dp.rand_obs = observations != 0;
+    h->params.latency = h->dp.latency = latency != 0;
     return SALP_OK;
 }
 

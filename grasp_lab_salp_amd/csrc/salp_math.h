@@ -273,6 +273,66 @@ SM_QUAL double sm_atan2(double y, double x) {
         default: return (z - pi_lo) - pi;
     }
 }
+/* ------------------------------------------------------------------ log */
+/* fdlibm __ieee754_log (e_log.c): argument reduction to [sqrt(2)/2, sqrt(2)]
+ * and the Lg1..Lg7 minimax polynomial in s = f / (2 + f).  Used by the
+ * Box-Muller draws of the disturbance noise (device and oracle alike). */
+SM_QUAL double sm_log(double x) {
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+                 two54 = 1.80143985094819840000e+16, Lg1 = 6.666666666666735130e-01,
+                 Lg2 = 3.999999999940941908e-01, Lg3 = 2.857142874366239149e-01,
+                 Lg4 = 2.222219843214978396e-01, Lg5 = 1.818357216161805012e-01,
+                 Lg6 = 1.531383769920937332e-01, Lg7 = 1.479819860511658591e-01;
+    uint64_t u = sm_d2u(x);
+    int32_t hx = (int32_t)(u >> 32);
+    uint32_t lx = (uint32_t)u;
+    int k = 0;
+    if (hx < 0x00100000) {                          /* x < 2^-1022 */
+        if (((hx & 0x7fffffff) | lx) == 0) return -INFINITY;
+        if (hx < 0) return NAN;
+        k -= 54;
+        x *= two54;
+        u = sm_d2u(x);
+        hx = (int32_t)(u >> 32);
+    }
+    if (hx >= 0x7ff00000) return x + x;
+    k += (hx >> 20) - 1023;
+    hx &= 0x000fffff;
+    int32_t i = (hx + 0x95f64) & 0x100000;
+    x = sm_u2d(((uint64_t)(uint32_t)(hx | (i ^ 0x3ff00000)) << 32) | (sm_d2u(x) & 0xffffffffu));
+    k += (i >> 20);
+    double f = x - 1.0;
+    double dk;
+    if ((0x000fffff & (2 + hx)) < 3) {              /* |f| < 2^-20 */
+        if (f == 0.0) {
+            if (k == 0) return 0.0;
+            dk = (double)k;
+            return dk * ln2_hi + dk * ln2_lo;
+        }
+        double R = f * f * (0.5 - 0.33333333333333333 * f);
+        if (k == 0) return f - R;
+        dk = (double)k;
+        return dk * ln2_hi - ((R - dk * ln2_lo) - f);
+    }
+    double s = f / (2.0 + f);
+    dk = (double)k;
+    double z = s * s;
+    i = hx - 0x6147a;
+    double w = z * z;
+    int32_t j = 0x6b851 - hx;
+    double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+    double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    i |= j;
+    double R = t2 + t1;
+    if (i > 0) {
+        double hfsq = 0.5 * f * f;
+        if (k == 0) return f - (hfsq - s * (hfsq + R));
+        return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+    }
+    if (k == 0) return f - s * (f - R);
+    return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
 SM_QUAL double sm_asin(double x) { return sm_atan2(x, sqrt((1.0 - x) * (1.0 + x))); }
 SM_QUAL double sm_acos(double x) { return sm_atan2(sqrt((1.0 - x) * (1.0 + x)), x); }
 

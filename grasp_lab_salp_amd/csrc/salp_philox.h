@@ -73,4 +73,26 @@ SP_QUAL void sp_reset_pair(uint64_t seed, uint64_t env_id, uint64_t episode, uin
     *u1 = sp_u01d(r.v[2], r.v[3]);
 }
 
+/* ------------------------------------------------ randomisation streams */
+/* Domain randomisation, disturbances, action / observation noise and latency
+ * (src/robot.py:210-242, 594-628, 796-800, 834-838; src/salp_robot_env.py:
+ * 176-194, 293-297) draw from NumPy's global MT19937 in the reference; here
+ * from Philox keyed by (seed, stream), counter (ctr, env id, group).  Device
+ * and oracle share this mapping, so they agree bit for bit; agreement with the
+ * reference is statistical (tests/test_randomization.py). */
+#define SP_STREAM_COEF 2u      /* Robot._randomize_parameters, per set_control    */
+#define SP_STREAM_NOISE 3u     /* OU disturbance increments, per physics tick     */
+#define SP_STREAM_ACTNOISE 4u  /* SalpRobotEnv._randomize_actions, per env-step   */
+#define SP_STREAM_OBSNOISE 5u  /* SalpRobotEnv._randomize_observations, per step  */
+#define SP_STREAM_LATENCY 6u   /* the latency set_control's coast time, per step  */
+
+SP_QUAL sp_u32x4 sp_draw(uint64_t seed, uint64_t env_id, uint64_t ctr, uint32_t stream, uint32_t group) {
+    return sp_philox4x32_10((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)env_id,
+                            ((uint32_t)(env_id >> 32) & 0xFFFFu) | (group << 16),
+                            (uint32_t)seed ^ (0x6C8E9CF5u * stream), (uint32_t)(seed >> 32) ^ stream);
+}
+/* float64 uniform in [0, 1) with 32 random bits (np.random.random_sample
+ * stand-in; distributional, not bitwise, parity with the reference). */
+SP_QUAL double sp_u01_32(uint32_t x) { return (double)x * 0x1.0p-32; }
+
 #endif /* SALP_PHILOX_H */

@@ -136,10 +136,20 @@ class Robot:
         self.density = density
 
     def enable_dynamic_randomization(self):
+        """src/robot.py:436-438: coefficients redrawn at every set_control."""
         self.dynamics_randomization = True
+        self._sync_randomization()
 
     def enable_disturbances(self):
+        """src/robot.py:440-441: OU force / torque disturbances every tick."""
         self.disturbances = True
+        self._sync_randomization()
+
+    def _sync_randomization(self):
+        if self._owner is not None:
+            self._owner._sync_randomization()
+        elif self._bound:
+            self._env.set_randomization(self.dynamics_randomization, self.disturbances)
 
     def enable_history_recording(self):
         self.record = True
@@ -153,10 +163,6 @@ class Robot:
 
     def salp_params(self, **env_kwargs):
         """The SalpParams the device needs for this robot (+ env arguments)."""
-        if self.dynamics_randomization or self.disturbances:
-            raise NotImplementedError(
-                "domain randomisation / OU disturbances (src/robot.py:210-242, 594-628) are not "
-                "implemented on the device yet; they are off in every reference script")
         n = self.nozzle
         return default_params(
             nozzle_length1=float(n.length1), nozzle_length2=float(n.length2),
@@ -164,7 +170,8 @@ class Robot:
             dry_mass=float(self.dry_mass), init_length=float(self.init_length),
             init_width=float(self.init_width), max_contraction=float(self.max_contraction),
             density=float(self.density), init_angle1=float(n._local["angle1"]),
-            init_angle2=float(n._local["angle2"]), **env_kwargs)
+            init_angle2=float(n._local["angle2"]), dynamics_randomization=int(self.dynamics_randomization),
+            disturbances=int(self.disturbances), **env_kwargs)
 
     # ----------------------------------------------------------- binding
     @property

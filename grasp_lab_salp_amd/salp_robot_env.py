@@ -14,10 +14,11 @@ Targets and obstacles are drawn on the host from the process-global
 (src/salp_robot_env.py:449-559), then handed to the device: seeding
 ``np.random`` reproduces the reference's episodes.
 
-Not on the device (fail loudly): pygame rendering / GIF recording / the
-interactive loop (visualisation, src/salp_robot_env.py:586-1595) and the
-action / observation randomisation and latency options (off in every
-reference script, src/salp_robot_env.py:54-56).
+The action / observation randomisation and latency options (off in every
+reference script, src/salp_robot_env.py:54-56) run on the device with Philox
+draws (grasp_lab_salp_amd/csrc/salp_random.h).  Not on the device (fail
+loudly): pygame rendering / GIF recording / the interactive loop
+(visualisation, src/salp_robot_env.py:586-1595).
 """
 from typing import Dict, Optional, Tuple
 
@@ -133,18 +134,24 @@ class SalpRobotEnv(GymEnv):
 
     # ------------------------------------------------------------ options
     def enable_action_randomization(self):
+        """src/salp_robot_env.py:157-158, 176-181 (device Philox draws)."""
         self.action_randomization = True
+        self._sync_randomization()
 
     def enable_observation_randomization(self):
+        """src/salp_robot_env.py:160-161, 183-194; the observation stays float32
+        (the reference's randomised observation is a float64 array)."""
         self.observation_randomization = True
+        self._sync_randomization()
 
     def enable_latency(self):
+        """src/salp_robot_env.py:163-164, 292-297."""
         self.latency = True
+        self._sync_randomization()
 
-    def _unsupported(self):
-        if self.action_randomization or self.observation_randomization or self.latency:
-            raise NotImplementedError("action/observation randomisation and latency "
-                                      "(src/salp_robot_env.py:157-194, 293-297) are not on the device yet")
+    def _sync_randomization(self):
+        self._sim.set_randomization(self.robot.dynamics_randomization, self.robot.disturbances,
+                                    self.action_randomization, self.observation_randomization, self.latency)
 
     # ------------------------------------------------------------ helpers
     def generate_target_point(self, strategy: str = "random", center=None, max_distance: float = 2.0):
@@ -206,7 +213,6 @@ class SalpRobotEnv(GymEnv):
 
     def step(self, action: np.ndarray) -> Tuple[np.ndarray, float, bool, bool, Dict]:
         """src/salp_robot_env.py:196-299: one breathing cycle on the device."""
-        self._unsupported()
         a = np.asarray(action, dtype=np.float32).reshape(3)   # SB3 passes the Box dtype
         self.action = a.copy()
         record = self.robot.record

@@ -49,8 +49,8 @@ def lib():
         L.oracle_robot_reset.argtypes = [sp, i64, P(d), P(u8)]
         L.oracle_nozzle_set_angles.argtypes = [sp, i64, P(d), P(d)]
         L.oracle_nozzle_solve.argtypes = [sp, i64, P(d), P(d), ctypes.c_int]
-        L.oracle_robot_set_control.argtypes = [sp, i64, P(d), P(d), ctypes.c_int]
-        L.oracle_robot_cycle.argtypes = [sp, i64, P(d), P(d), i64, P(i64), P(i64)]
+        L.oracle_robot_set_control.argtypes = [sp, i64, P(d), P(d), ctypes.c_int, ctypes.c_uint64, i64]
+        L.oracle_robot_cycle.argtypes = [sp, i64, P(d), P(d), i64, P(i64), P(i64), ctypes.c_uint64, i64]
         L.oracle_philox.argtypes = [u32] * 6 + [P(u32)]
         if L.oracle_num_fields() != NUM_FIELDS:
             raise RuntimeError("oracle / _abi field count mismatch")
@@ -136,7 +136,7 @@ class Oracle:
         c = np.ascontiguousarray(control, np.float64).reshape(self.n, 4)
         lib().oracle_robot_set_control(ctypes.byref(self.params), self.n,
                                        _p(self.state, ctypes.c_double), _p(c, ctypes.c_double),
-                                       int(bool(contraction_f32)))
+                                       int(bool(contraction_f32)), self.seed, self.env_offset)
 
     def robot_cycle(self, max_samples=0):
         """step_through_cycle; returns (ticks [n], rows [max_samples, DIM, n] or
@@ -148,8 +148,18 @@ class Oracle:
             ns = np.zeros(self.n, np.int64)
         lib().oracle_robot_cycle(ctypes.byref(self.params), self.n, _p(self.state, ctypes.c_double),
                                  _p(rows, ctypes.c_double), int(max_samples),
-                                 _p(ns, ctypes.c_int64), _p(ticks, ctypes.c_int64))
+                                 _p(ns, ctypes.c_int64), _p(ticks, ctypes.c_int64), self.seed,
+                                 self.env_offset)
         return ticks, rows, ns
+
+    def set_randomization(self, dynamics=False, disturbances=False, actions=False, observations=False,
+                          latency=False):
+        """The reference's enable_* switches (include/salp.h SalpParams)."""
+        p = SalpParams.from_buffer_copy(self.params)
+        p.dynamics_randomization, p.disturbances = int(bool(dynamics)), int(bool(disturbances))
+        p.action_randomization, p.observation_randomization = int(bool(actions)), int(bool(observations))
+        p.latency = int(bool(latency))
+        self.params = p
 
     def step_random(self, n_steps, threads=0):
         rs = np.zeros(self.n, np.float64)

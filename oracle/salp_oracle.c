@@ -30,6 +30,7 @@
 #include "../include/salp.h"
 #include "../grasp_lab_salp_amd/csrc/salp_math.h"
 #include "../grasp_lab_salp_amd/csrc/salp_philox.h"
+#include "../grasp_lab_salp_amd/csrc/salp_random.h"
 
 #ifdef _OPENMP
 #include <omp.h>
@@ -212,9 +213,17 @@ typedef struct {
     /* physical parameters src/robot.py:285-295 */
     double dry_mass, buoy_mass, skin_mass, tube_mass, init_length, init_width, max_contraction;
     double density, tube_volume;
-    /* coefficients src/robot.py:300-308 (means; randomisation is off) */
+    /* coefficients src/robot.py:300-308 (means, or the draw of
+     * Robot._randomize_parameters :594-628 when dynamics randomisation is on) */
     double discharge_coefficient, drag_force_ratio, drag_torque_ratio;
     M3 amf, amrf, amt, amrt;
+    /* randomisation switches (SalpParams) and their Philox stream
+     * (grasp_lab_salp_amd/csrc/salp_random.h): seed, global env id, the
+     * set_control and tick counters, OUDisturbance states src/robot.py:210-242 */
+    int rand_dyn, rand_dist, rand_act, rand_obs, latency;
+    uint64_t seed, env_id;
+    double rng_ctl, rng_tick;
+    V3 ou_force, ou_torque;
     double trans_range[3][2], rot_range[3][2];
     /* control src/robot.py:311-316 */
     double contraction, contract_rate, release_rate, refill_time, jet_time, coast_time;
@@ -593,6 +602,9 @@ static void robot_init(Obj* o, const SalpParams* p) {
     o->num_obstacles = p->num_obstacles; o->obstacle_radius = p->obstacle_radius;
     o->max_cycles = p->max_cycles;
     o->tank_margin = 50; o->target_radius = 0.2;
+    o->rand_dyn = p->dynamics_randomization != 0; o->rand_dist = p->disturbances != 0;
+    o->rand_act = p->action_randomization != 0; o->rand_obs = p->observation_randomization != 0;
+    o->latency = p->latency != 0;
 }
 
 /* src/robot.py:452-501 */
@@ -619,11 +631,30 @@ static void robot_reset(Obj* o) {
     o->prev_I = r_get_inertia(o);
     o->tcd = r_trans_cd(o);
     o->rcd = r_rot_cd(o);
+    o->ou_force = vzero();             /* force_disturbance.reset() :454 */
+    o->ou_torque = vzero();            /* torque_disturbance.reset() :455 */
 }
 
-/* src/robot.py:544-592 (dynamics_randomization off) */
+/* src/robot.py:553-561 / 594-628 */
+static void robot_coefficients(Obj* o) {
+    SrCoef k;
+    if (o->rand_dyn) {
+        sr_draw_coefs(o->seed, o->env_id, (uint64_t)o->rng_ctl, &k);
+        o->rng_ctl += 1.0;
+    } else {
+        sr_coef_means(&k);
+    }
+    o->discharge_coefficient = k.cd; o->drag_force_ratio = k.dfr; o->drag_torque_ratio = k.dtr;
+    o->amf = mdiag(k.amf[0], k.amf[1], k.amf[2]);
+    o->amrf = mdiag(k.amrf[0], k.amrf[1], k.amrf[2]);
+    o->amt = mdiag(k.amt[0], k.amt[1], k.amt[2]);
+    o->amrt = mdiag(k.amrt[0], k.amrt[1], k.amrt[2]);
+}
+
+/* src/robot.py:544-592 */
 static void robot_set_control(Obj* o, double contraction, double coast_time, double a1, double a2,
                               int c32) {
+    robot_coefficients(o);
     o->avg_v = vzero(); o->avg_w = vzero();
     o->contraction = contraction; o->coast_time = coast_time;
     o->c32 = c32;
@@ -681,6 +712,18 @@ static V3 robot_newton(Obj* o) {
     o->added_mass_force = compute_added_mass_force(o->mass, o->amf, o->mass_rate, o->amrf, o->acc,
                                                    o->w, o->v);
     V3 noise = vzero();
+    if (o->rand_dist) {
+        /* force_disturbance.sample(), then force_noise[-1] = 0 zeroes the
+         * process's own z state (the array is shared); the torque process is
+         * stepped with the same tick's draws (its x, y are zeroed likewise) */
+        double z0, z1, z2;
+        sr_normals3(o->seed, o->env_id, (uint64_t)o->rng_tick, &z0, &z1, &z2);
+        o->rng_tick += 1.0;
+        o->ou_force = v3(sr_ou_step(o->ou_force.v[0], SR_OU_FORCE_THETA, SR_OU_FORCE_SIGMA, z0),
+                         sr_ou_step(o->ou_force.v[1], SR_OU_FORCE_THETA, SR_OU_FORCE_SIGMA, z1), 0.0);
+        o->ou_torque = v3(0.0, 0.0, sr_ou_step(o->ou_torque.v[2], SR_OU_TORQUE_THETA, SR_OU_TORQUE_SIGMA, z2));
+        noise = o->ou_force;
+    }
     o->mass = r_get_mass(o);
     V3 a_tan = cross(o->alpha, o->com);
     V3 a_cen = cross(o->w, cross(o->w, o->com));
@@ -704,7 +747,7 @@ static V3 robot_euler(Obj* o) {
     M3 Ir_a = r_get_inertia_rate(o); /* prev_I was just updated: exactly zero */
     o->added_mass_torque = compute_added_mass_torque(I_a, o->amt, Ir_a, o->amrt, r_get_mass(o),
                                                      o->amf, o->alpha, o->w, o->v);
-    V3 noise = vzero();
+    V3 noise = o->rand_dist ? o->ou_torque : vzero();
     M3 I = r_get_inertia(o);
     V3 total = vadd(vadd(vadd(vadd(vadd(vadd(o->jet_torque, o->drag_torque), o->coriolis_torque),
                                         o->asymmetry_torque), o->deform_torque),
@@ -890,9 +933,17 @@ static int64_t env_begin_and_run_cycle(Obj* o, const float* action) {
     o->action[0] = action[0]; o->action[1] = action[1]; o->action[2] = action[2];
     float r[3];
     env_rescale_action(action, r);
-    nozzle_set_yaw_angle(&o->nz, (double)r[2]);
-    nozzle_solve_angles(&o->nz, 1);
-    robot_set_control(o, (double)r[0], (double)r[1], o->nz.angle1, o->nz.angle2, 1);
+    if (o->rand_act) {   /* _randomize_actions (:176-181): Python floats from here */
+        double ra[3];
+        sr_randomize_action(o->seed, o->env_id, (uint64_t)o->step_count, r, ra);
+        nozzle_set_yaw_angle(&o->nz, ra[2]);
+        nozzle_solve_angles(&o->nz, 0);
+        robot_set_control(o, ra[0], ra[1], o->nz.angle1, o->nz.angle2, 0);
+    } else {
+        nozzle_set_yaw_angle(&o->nz, (double)r[2]);
+        nozzle_solve_angles(&o->nz, 1);
+        robot_set_control(o, (double)r[0], (double)r[1], o->nz.angle1, o->nz.angle2, 1);
+    }
     return robot_step_through_cycle(o, NULL, 0, 0, NULL);
 }
 
@@ -952,6 +1003,7 @@ static double env_finish_step(Obj* o, float* obs, uint8_t* term_out, uint8_t* tr
     double comp[7];
     double reward = env_reward(o, comp);
     env_observation(o, obs);
+    if (o->rand_obs) sr_randomize_obs(o->seed, o->env_id, (uint64_t)o->step_count, obs);  /* :253-254 */
     int hit = env_hit_obstacle(o);
     int done = 0, truncated = 0;
     if (dist < o->target_radius) { done = 1; reward += 500.0; }
@@ -988,6 +1040,10 @@ static double env_finish_step(Obj* o, float* obs, uint8_t* term_out, uint8_t* tr
     }
     o->prev_a2 = (double)o->action[2];
     o->pending = 0;
+    if (o->latency) {    /* src/salp_robot_env.py:292-297 */
+        double lat = sr_latency(o->seed, o->env_id, (uint64_t)o->step_count);
+        robot_set_control(o, 0.0, lat, o->nz.angle1, o->nz.angle2, 0);
+    }
     *term_out = (uint8_t)done;
     *trunc_out = (uint8_t)truncated;
     return reward;
@@ -1065,12 +1121,28 @@ static void obj_pack(const Obj* o, double* s, int64_t n, int64_t i) {
     F(s, SALP_F_PENDING, n, i) = o->pending;
     F(s, SALP_F_STEP_COUNT, n, i) = o->step_count;
     F(s, SALP_F_EPISODE, n, i) = o->episode;
+    F(s, SALP_F_CD, n, i) = o->discharge_coefficient;
+    F(s, SALP_F_DFR, n, i) = o->drag_force_ratio;
+    F(s, SALP_F_DTR, n, i) = o->drag_torque_ratio;
+    for (int k = 0; k < 3; ++k) {
+        F(s, SALP_F_AMF0 + k, n, i) = o->amf.m[k][k];
+        F(s, SALP_F_AMRF0 + k, n, i) = o->amrf.m[k][k];
+        F(s, SALP_F_AMT0 + k, n, i) = o->amt.m[k][k];
+        F(s, SALP_F_AMRT0 + k, n, i) = o->amrt.m[k][k];
+        F(s, SALP_F_OUF0 + k, n, i) = o->ou_force.v[k];
+        F(s, SALP_F_OUT0 + k, n, i) = o->ou_torque.v[k];
+    }
+    F(s, SALP_F_RNG_CTL, n, i) = o->rng_ctl;
+    F(s, SALP_F_RNG_TICK, n, i) = o->rng_tick;
 }
 
 /* Rebuild the full reference object from the minimal state.  Every derived
  * attribute is a pure function of stored ones at an env-step boundary. */
-static void obj_unpack(Obj* o, const SalpParams* p, const double* s, int64_t n, int64_t i) {
+static void obj_unpack(Obj* o, const SalpParams* p, const double* s, int64_t n, int64_t i, uint64_t seed,
+                       int64_t env_offset) {
     robot_init(o, p);
+    o->seed = seed;
+    o->env_id = (uint64_t)(env_offset + i);
     for (int k = 0; k < 3; ++k) {
         o->v.v[k] = F(s, SALP_F_V0 + k, n, i);
         o->w.v[k] = F(s, SALP_F_W0 + k, n, i);
@@ -1153,6 +1225,17 @@ static void obj_unpack(Obj* o, const SalpParams* p, const double* s, int64_t n, 
     o->pending = (int)F(s, SALP_F_PENDING, n, i);
     o->step_count = F(s, SALP_F_STEP_COUNT, n, i);
     o->episode = F(s, SALP_F_EPISODE, n, i);
+    o->discharge_coefficient = F(s, SALP_F_CD, n, i);
+    o->drag_force_ratio = F(s, SALP_F_DFR, n, i);
+    o->drag_torque_ratio = F(s, SALP_F_DTR, n, i);
+    o->amf = mdiag(F(s, SALP_F_AMF0, n, i), F(s, SALP_F_AMF1, n, i), F(s, SALP_F_AMF2, n, i));
+    o->amrf = mdiag(F(s, SALP_F_AMRF0, n, i), F(s, SALP_F_AMRF1, n, i), F(s, SALP_F_AMRF2, n, i));
+    o->amt = mdiag(F(s, SALP_F_AMT0, n, i), F(s, SALP_F_AMT1, n, i), F(s, SALP_F_AMT2, n, i));
+    o->amrt = mdiag(F(s, SALP_F_AMRT0, n, i), F(s, SALP_F_AMRT1, n, i), F(s, SALP_F_AMRT2, n, i));
+    o->ou_force = v3(F(s, SALP_F_OUF0, n, i), F(s, SALP_F_OUF1, n, i), F(s, SALP_F_OUF2, n, i));
+    o->ou_torque = v3(F(s, SALP_F_OUT0, n, i), F(s, SALP_F_OUT1, n, i), F(s, SALP_F_OUT2, n, i));
+    o->rng_ctl = F(s, SALP_F_RNG_CTL, n, i);
+    o->rng_tick = F(s, SALP_F_RNG_TICK, n, i);
 }
 
 /* --------------------------------------------------------- exported API */
@@ -1174,11 +1257,13 @@ int oracle_init(const SalpParams* p, int64_t n, double* state) {
 int oracle_reset_to(const SalpParams* p, int64_t n, double* state, const uint8_t* mask,
                     const float* targets, const float* obstacles, const int32_t* n_obst,
                     float* obs_out, int obs_dim) {
+    const uint64_t seed = 0;
+    const int64_t env_offset = 0;
 #pragma omp parallel for schedule(dynamic, 16)
     for (int64_t i = 0; i < n; ++i) {
         if (mask && !mask[i]) continue;
         Obj o;
-        obj_unpack(&o, p, state, n, i);
+        obj_unpack(&o, p, state, n, i, seed, env_offset);
         env_reset_with(&o, targets + 2 * i, obstacles + 2 * SALP_MAX_OBSTACLES * i, n_obst[i],
                        obs_out ? obs_out + (size_t)obs_dim * i : NULL);
         obj_pack(&o, state, n, i);
@@ -1192,7 +1277,7 @@ int oracle_reset(const SalpParams* p, int64_t n, double* state, const uint8_t* m
     for (int64_t i = 0; i < n; ++i) {
         if (mask && !mask[i]) continue;
         Obj o;
-        obj_unpack(&o, p, state, n, i);
+        obj_unpack(&o, p, state, n, i, seed, env_offset);
         float tgt[2], obst[2 * SALP_MAX_OBSTACLES];
         int nob;
         env_draw_reset(&o, seed, (uint64_t)(env_offset + i), tgt, obst, &nob);
@@ -1210,7 +1295,7 @@ int oracle_step(const SalpParams* p, int64_t n, double* state, const float* acti
 #pragma omp parallel for schedule(dynamic, 4)
     for (int64_t i = 0; i < n; ++i) {
         Obj o;
-        obj_unpack(&o, p, state, n, i);
+        obj_unpack(&o, p, state, n, i, seed, env_offset);
         float obs[SALP_OBS_DIM_MAX];
         uint8_t te, tr;
         int64_t ticks = env_begin_and_run_cycle(&o, actions + 3 * i);
@@ -1246,7 +1331,7 @@ int64_t oracle_step_random(const SalpParams* p, int64_t n, double* state, int32_
 #pragma omp parallel for schedule(dynamic, 1) reduction(+ : total_ticks)
     for (int64_t i = 0; i < n; ++i) {
         Obj o;
-        obj_unpack(&o, p, state, n, i);
+        obj_unpack(&o, p, state, n, i, seed, env_offset);
         double rs = 0.0;
         for (int32_t k = 0; k < n_steps; ++k) {
             float a[3], obs[SALP_OBS_DIM_MAX];
@@ -1311,10 +1396,12 @@ int64_t oracle_robot_trace(const SalpParams* p, const float* actions, int n_acti
 
 /* Robot / Nozzle level (include/salp.h salp_robot_*, salp_nozzle_*). */
 int oracle_robot_reset(const SalpParams* p, int64_t n, double* state, const uint8_t* mask) {
+    const uint64_t seed = 0;
+    const int64_t env_offset = 0;
     for (int64_t i = 0; i < n; ++i) {
         if (mask && !mask[i]) continue;
         Obj o;
-        obj_unpack(&o, p, state, n, i);
+        obj_unpack(&o, p, state, n, i, seed, env_offset);
         robot_reset(&o);
         o.pending = 0;
         obj_pack(&o, state, n, i);
@@ -1322,28 +1409,33 @@ int oracle_robot_reset(const SalpParams* p, int64_t n, double* state, const uint
     return 0;
 }
 int oracle_nozzle_set_angles(const SalpParams* p, int64_t n, double* state, const double* ang) {
+    const uint64_t seed = 0;
+    const int64_t env_offset = 0;
     for (int64_t i = 0; i < n; ++i) {
         Obj o;
-        obj_unpack(&o, p, state, n, i);
+        obj_unpack(&o, p, state, n, i, seed, env_offset);
         nozzle_set_angles(&o.nz, ang[2 * i], ang[2 * i + 1]);
         obj_pack(&o, state, n, i);
     }
     return 0;
 }
 int oracle_nozzle_solve(const SalpParams* p, int64_t n, double* state, const double* yaw, int yaw32) {
+    const uint64_t seed = 0;
+    const int64_t env_offset = 0;
     for (int64_t i = 0; i < n; ++i) {
         Obj o;
-        obj_unpack(&o, p, state, n, i);
+        obj_unpack(&o, p, state, n, i, seed, env_offset);
         nozzle_set_yaw_angle(&o.nz, yaw[i]);
         nozzle_solve_angles(&o.nz, yaw32);
         obj_pack(&o, state, n, i);
     }
     return 0;
 }
-int oracle_robot_set_control(const SalpParams* p, int64_t n, double* state, const double* ctl, int c32) {
+int oracle_robot_set_control(const SalpParams* p, int64_t n, double* state, const double* ctl, int c32,
+                             uint64_t seed, int64_t env_offset) {
     for (int64_t i = 0; i < n; ++i) {
         Obj o;
-        obj_unpack(&o, p, state, n, i);
+        obj_unpack(&o, p, state, n, i, seed, env_offset);
         robot_set_control(&o, ctl[4 * i], ctl[4 * i + 1], ctl[4 * i + 2], ctl[4 * i + 3], c32);
         obj_pack(&o, state, n, i);
     }
@@ -1352,11 +1444,12 @@ int oracle_robot_set_control(const SalpParams* p, int64_t n, double* state, cons
 /* step_through_cycle for every env; rows/n_samples may be NULL (no record).
  * ticks_out [n] may be NULL. */
 int oracle_robot_cycle(const SalpParams* p, int64_t n, double* state, double* rows,
-                       int64_t max_samples, int64_t* n_samples, int64_t* ticks_out) {
+                       int64_t max_samples, int64_t* n_samples, int64_t* ticks_out, uint64_t seed,
+                       int64_t env_offset) {
 #pragma omp parallel for schedule(dynamic, 4)
     for (int64_t i = 0; i < n; ++i) {
         Obj o;
-        obj_unpack(&o, p, state, n, i);
+        obj_unpack(&o, p, state, n, i, seed, env_offset);
         int64_t t = robot_step_through_cycle(&o, rows ? rows + i : NULL, n, max_samples,
                                              n_samples ? n_samples + i : NULL);
         o.pending = 0;

@@ -64,8 +64,9 @@ def test_make_env_configuration_capture():
     assert nozzle.turn_time == pytest.approx((0.3 + 0.2) / (31 * np.pi / 30))
     assert robot.salp_params().init_angle1 == 0.3
     robot.enable_disturbances()
-    with pytest.raises(NotImplementedError):
-        robot.salp_params()
+    robot.enable_dynamic_randomization()
+    q = robot.salp_params()
+    assert q.disturbances == 1 and q.dynamics_randomization == 1 and q.latency == 0
 
 
 def test_phase_enum_mirrors_reference():
