@@ -348,12 +348,24 @@ struct Hot {
  * register copy of one env's row (ColdRegs*, the rollout boundary) so that the
  * env-step epilogue/prologue issues all its loads at once instead of one
  * dependent HBM round trip per read-modify-write. */
-struct ColdRegs { double v[SALP_NUM_FIELDS]; };
+/* RAND = false: the randomisation fields (SALP_F_CD and after) are not
+ * cached; the plain kernels only ever store constants into them (coefficient
+ * means, calm OU states), so they pass straight through to HBM and cost no
+ * registers. */
+template <bool RAND>
+struct ColdRegs {
+    double v[SALP_NUM_FIELDS];
+    double* g;   /* this env's column of the HBM state: g[f * n] */
+    int64_t n;
+};
 SD double& sref(double* S, const Params& P, int64_t i, int f) { return S[(size_t)f * (size_t)P.n + (size_t)i]; }
 SD const double& sref(const double* S, const Params& P, int64_t i, int f) {
     return S[(size_t)f * (size_t)P.n + (size_t)i];
 }
-SD double& sref(ColdRegs* C, const Params&, int64_t, int f) { return C->v[f]; }
+template <bool RAND>
+SD double& sref(ColdRegs<RAND>* C, const Params&, int64_t, int f) {
+    return (!RAND && f >= SALP_F_CD) ? C->g[(size_t)f * (size_t)C->n] : C->v[f];
+}
 #define SF(f) sref(S, P, i, (f))
 
 /* Register-resident values derived from the stored state: geometry of the
@@ -708,9 +720,13 @@ SD double nozzle_set_angles(ST S, const Params& P, int64_t i, double a1, double 
 /* Robot.set_control (src/robot.py:544-592, geometry.py:14-26); c32: the
  * contraction is an np.float32 (contraction**2 is then float32). */
 /* this cycle's coefficients: Robot._randomize_parameters (src/robot.py:
- * 594-628) when dynamics randomisation is on, else the means (:553-561) */
+ * 594-628) when dynamics randomisation is on, else the means (:553-561).
+ * The plain kernels run only with every switch off, when the stored
+ * coefficients are the means already (salp_set_randomization restores them
+ * when the switch goes off), so they skip this. */
 template <bool RAND, class ST>
 SD void set_coefficients(Hot& h, ST S, const Params& P, int64_t i) {
+    if (!RAND) return;
     SrCoef k;
     if (RAND && P.rand_dyn) {
         sr_draw_coefs(P.seed, h.env_id, (uint64_t)SF(SALP_F_RNG_CTL), &k);
@@ -1056,10 +1072,13 @@ SD void robot_reset(Hot& h, ST S, const Params& P, int64_t i) {
     h.pV = h.V; h.pv32 = false;
     refresh_derived(h, P);
     h.pI0 = h.geo.I0; h.pI1 = h.geo.I1; h.pI2 = h.geo.I1;
-    /* force_disturbance.reset(), torque_disturbance.reset() (src/robot.py:454-455) */
-    SF(SALP_F_OUF0) = 0.0; SF(SALP_F_OUF1) = 0.0; SF(SALP_F_OUF2) = 0.0;
-    SF(SALP_F_OUT0) = 0.0; SF(SALP_F_OUT1) = 0.0; SF(SALP_F_OUT2) = 0.0;
-    h.rnd.ouf0 = 0.0; h.rnd.ouf1 = 0.0; h.rnd.out2 = 0.0;
+    /* force_disturbance.reset(), torque_disturbance.reset() (src/robot.py:454-455);
+     * with disturbances off the processes are calm already (salp_set_randomization) */
+    if (P.rand_dist) {
+        SF(SALP_F_OUF0) = 0.0; SF(SALP_F_OUF1) = 0.0; SF(SALP_F_OUF2) = 0.0;
+        SF(SALP_F_OUT0) = 0.0; SF(SALP_F_OUT1) = 0.0; SF(SALP_F_OUT2) = 0.0;
+        h.rnd.ouf0 = 0.0; h.rnd.ouf1 = 0.0; h.rnd.out2 = 0.0;
+    }
     SF(SALP_F_PENDING) = 0.0;
 }
 
@@ -1120,16 +1139,20 @@ SD constexpr bool is_hot(int f) {
 }
 /* One env's cold fields into registers with all loads in flight at once. */
 template <bool RAND>
-SD void load_cold(ColdRegs& C, const double* S, const Params& P, int64_t i) {
+SD constexpr bool is_cached(int f) { return !is_hot<RAND>(f) && (RAND || f < SALP_F_CD); }
+template <bool RAND>
+SD void load_cold(ColdRegs<RAND>& C, double* S, const Params& P, int64_t i) {
+    C.g = S + i;
+    C.n = P.n;
 #pragma unroll
     for (int f = 0; f < SALP_NUM_FIELDS; ++f)
-        if (!is_hot<RAND>(f)) C.v[f] = S[(size_t)f * (size_t)P.n + (size_t)i];
+        if (is_cached<RAND>(f)) C.v[f] = S[(size_t)f * (size_t)P.n + (size_t)i];
 }
 template <bool RAND>
-SD void store_cold(const ColdRegs& C, double* S, const Params& P, int64_t i) {
+SD void store_cold(const ColdRegs<RAND>& C, double* S, const Params& P, int64_t i) {
 #pragma unroll
     for (int f = 0; f < SALP_NUM_FIELDS; ++f)
-        if (!is_hot<RAND>(f)) S[(size_t)f * (size_t)P.n + (size_t)i] = C.v[f];
+        if (is_cached<RAND>(f)) S[(size_t)f * (size_t)P.n + (size_t)i] = C.v[f];
 }
 
 /* A lane's slot of a workgroup LDS array [SPILL_N][LANES]: the whole Hot
@@ -1188,6 +1211,22 @@ SD void unspill(Hot& h, SpillSlot s, const Params& P, uint64_t env_id) {
         h.geo.speed = v[61]; h.geo.rx = v[62];
     }
     cycle_bounds(h);
+}
+
+/* Switching a randomisation feature off (an extension: the reference only
+ * has enable_*): coefficients back to the means, OU processes calm. */
+SD void calm_env(double* S, const Params& P, int64_t i, bool coefficients, bool ou) {
+    if (coefficients) {
+        SrCoef k;
+        sr_coef_means(&k);
+        SF(SALP_F_CD) = k.cd; SF(SALP_F_DFR) = k.dfr; SF(SALP_F_DTR) = k.dtr;
+        for (int j = 0; j < 3; ++j) {
+            SF(SALP_F_AMF0 + j) = k.amf[j]; SF(SALP_F_AMRF0 + j) = k.amrf[j];
+            SF(SALP_F_AMT0 + j) = k.amt[j]; SF(SALP_F_AMRT0 + j) = k.amrt[j];
+        }
+    }
+    if (ou)
+        for (int j = 0; j < 3; ++j) { SF(SALP_F_OUF0 + j) = 0.0; SF(SALP_F_OUT0 + j) = 0.0; }
 }
 
 /* Robot / Nozzle / SalpRobotEnv constructors (src/robot.py:20-47, 261-412) */

@@ -256,7 +256,7 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
                 const uint64_t env_id = (uint64_t)(a.P.env_offset + i);
                 Hot hb;
                 salp::unspill<RAND>(hb, sp, a.P, env_id);
-                salp::ColdRegs C;
+                salp::ColdRegs<RAND> C;
                 salp::load_cold<RAND>(C, a.S, a.P, i);
                 rollout_boundary<RAND>(hb, &C, a.P, i, env_id, pending, active, steps, a.max_steps, a.B, c32);
                 salp::store_cold<RAND>(C, a.S, a.P, i);
@@ -279,6 +279,12 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
 }
 
 // ------------------------------------------------ Robot / Nozzle level
+__global__ __launch_bounds__(kBlock) void k_calm(double* S, Params P, int coefficients, int ou) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    salp::calm_env(S, P, i, coefficients != 0, ou != 0);
+}
+
 __global__ __launch_bounds__(kBlock) void k_robot_reset(double* S, Params P, const uint8_t* mask) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.n || (mask && !mask[i])) return;
@@ -636,6 +642,16 @@ int salp_set_trace(SalpEnv* h, const SalpTraceBuffer* buf) {
 int salp_set_randomization(SalpEnv* h, int dynamics, int disturbances, int actions, int observations,
                            int latency) {
     if (!h) return fail(nullptr, SALP_EINVAL, "salp_set_randomization: null handle");
+    // a feature switched off leaves the reference's defaults behind: mean
+    // coefficients, calm disturbance processes (what the plain kernels assume)
+    const bool calm_coef = h->dp.rand_dyn && !dynamics, calm_ou = h->dp.rand_dist && !disturbances;
+    if (calm_coef || calm_ou) {
+        hipLaunchKernelGGL(k_calm, dim3(blocks_for(h->n)), dim3(kBlock), 0, nullptr, h->state, h->dp,
+                           (int)calm_coef, (int)calm_ou);
+        int rc = launched(h, "k_calm");
+        if (rc) return rc;
+        if ((rc = check_hip(h, hipDeviceSynchronize(), "salp_set_randomization sync"))) return rc;
+    }
     h->params.dynamics_randomization = h->dp.rand_dyn = dynamics != 0;
     h->params.disturbances = h->dp.rand_dist = disturbances != 0;
     h->params.action_randomization = h->dp.rand_act = actions != 0;

@@ -209,7 +209,10 @@ int salp_set_randomization(SalpEnv* h, int dynamics, int disturbances, int actio
 /* --------------------------------------------------------- state access */
 /* State is a struct-of-arrays of SALP_NUM_FIELDS fp64 rows of n_envs each:
  * state[field * n_envs + env].  Integer and float32 quantities are stored
- * exactly as doubles. */
+ * exactly as doubles.  With every randomisation switch off the coefficient
+ * fields hold the reference's means and the OU fields zero; the kernels then
+ * use the constants and leave those fields alone, so a state written with
+ * salp_set_state should keep them that way. */
 int salp_num_fields(void);
 const char* salp_field_name(int field);
 int salp_trace_dim(void);   /* SALP_TRACE_DIM */

@@ -154,7 +154,22 @@ class Oracle:
 
     def set_randomization(self, dynamics=False, disturbances=False, actions=False, observations=False,
                           latency=False):
-        """The reference's enable_* switches (include/salp.h SalpParams)."""
+        """The reference's enable_* switches (include/salp.h SalpParams).
+        Switching a feature off restores the reference's defaults (mean
+        coefficients, calm OU processes), as salp_set_randomization does."""
+        from grasp_lab_salp_amd._abi import FIELD
+        if self.params.dynamics_randomization and not dynamics:
+            means = {"cd": 0.3, "dfr": 0.25, "dtr": 0.1, "amf0": 0.5, "amf1": 0.6, "amf2": 0.6,
+                     "amt0": 0.3, "amt1": 0.6, "amt2": 0.6}
+            for j in range(3):
+                means[f"amrf{j}"] = 0.2
+                means[f"amrt{j}"] = 0.2
+            for k, v in means.items():
+                self.state[FIELD[k]] = v
+        if self.params.disturbances and not disturbances:
+            for j in range(3):
+                self.state[FIELD[f"ouf{j}"]] = 0.0
+                self.state[FIELD[f"out{j}"]] = 0.0
         p = SalpParams.from_buffer_copy(self.params)
         p.dynamics_randomization, p.disturbances = int(bool(dynamics)), int(bool(disturbances))
         p.action_randomization, p.observation_randomization = int(bool(actions)), int(bool(observations))

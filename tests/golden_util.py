@@ -58,6 +58,12 @@ def snapshot_to_state(d, prefix, rows):
     pI = g("r_prev_I")
     for i in range(3):
         s[FIELD[f"prev_I{i}"]] = pI[:, i]
+    # coefficients of the reference robot with randomisation off (src/robot.py:300-306)
+    for k, v in (("cd", 0.3), ("dfr", 0.25), ("dtr", 0.1), ("amf0", 0.5), ("amf1", 0.6), ("amf2", 0.6),
+                 ("amt0", 0.3), ("amt1", 0.6), ("amt2", 0.6)):
+        s[FIELD[k]] = v
+    for i in range(3):
+        s[FIELD[f"amrf{i}"]] = s[FIELD[f"amrt{i}"]] = 0.2
     s[FIELD["geom32"]] = g("r_len_is_f32")
     # env path: set_control always receives the float32 rescaled action
     s[FIELD["contr32"]] = 1.0
