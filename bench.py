@@ -26,13 +26,17 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from grasp_lab_salp_amd._abi import NUM_FIELDS, default_params  # noqa: E402
+from grasp_lab_salp_amd._abi import FIELD, default_params  # noqa: E402
 from grasp_lab_salp_amd.shard import env_id_offset, reduce_run  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X fp64 vector spec (half the 157.3 TF fp32 rate)
-STATE_BYTES = NUM_FIELDS * 8
+# compulsory bytes per env-step B = 2 * S + outputs, S = the
+# persistent per-env state an env-step reads and writes.  Here S = the 102
+# fields before the randomisation block (the plain path never touches those).
+STATE_BYTES = FIELD["cd"] * 8
 STEP_OUT_BYTES = 10 * 4 + 3 * 4 + 4 + 1   # obs + action + reward(f32) + done per env-step
+BYTES_PER_ENV_STEP = 2 * STATE_BYTES + STEP_OUT_BYTES
 
 
 def pmc_profile(n, budget, chunk):
@@ -152,7 +156,7 @@ def main():
     prof = pmc_profile(n, a.tick_budget, a.chunk)
     ticks_total = float(-(-a.tick_budget // a.chunk) * a.chunk) * n * a.steps * world
     steps_per_launch = steps_local / a.steps
-    bytes_launch = n * (2 * STATE_BYTES + 16) + steps_per_launch * STEP_OUT_BYTES
+    bytes_launch = steps_per_launch * BYTES_PER_ENV_STEP
     achieved = bytes_launch / (kern_ms / 1e3) / 1e9
     res = {
         "metric": "env-steps/sec at 65536 parallel envs, 1/2/4/8 MI355X; % HBM roofline",
@@ -179,8 +183,9 @@ def main():
                      "traffic": prof[1]["derived"].get("hbm_bytes") if prof else None,
                      "traffic_source": prof[0] if prof else None,
                      "bytes_per_launch": bytes_launch,
-                     "note": "algorithmic bytes = n*(2*state+16) + env-steps*57 per launch; the "
-                             "kernel is fp64-VALU bound (see roofline_valu)"},
+                     "bytes_per_env_step": BYTES_PER_ENV_STEP,
+                     "note": "algorithmic bytes = env-steps per launch x (2 x 816 B state + 57 B outputs) "
+                             "(SURVEY 8(d)); the kernel is fp64-VALU bound (see roofline_valu)"},
         "lockstep_env_steps_per_sec": lock_total,
     }
     f_tick = prof[1]["derived"].get("fp64_flops_per_env_tick") if prof else None
