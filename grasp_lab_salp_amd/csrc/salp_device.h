@@ -76,6 +76,17 @@ struct Params {
     uint64_t seed;
 };
 
+/* The launch constants the tick reads, moved into VGPRs for the tick loop
+ * (see sm_vconst: the kernel arguments otherwise hold SGPRs the loop needs
+ * for its fp64 constants).  Values unchanged. */
+SD Params pin_params(const Params& P) {
+    Params v = P;
+    asm volatile("" : "+v"(v.L0), "+v"(v.W0), "+v"(v.dry_mass), "+v"(v.nozzle_mass), "+v"(v.density),
+                 "+v"(v.nozzle_area), "+v"(v.mid_x), "+v"(v.tube_volume), "+v"(v.net_tube_mass),
+                 "+v"(v.com_mass_sum), "+v"(v.P1000tv), "+v"(v.end_aspect), "+v"(v.aspect_den));
+    return v;
+}
+
 /* ----------------------------------------------------------- helpers */
 SD double pymax(double a, double b) { return b > a ? b : a; }
 /* x / DT, correctly rounded, in 4 instructions instead of the ~11 of a general

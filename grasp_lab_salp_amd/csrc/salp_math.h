@@ -73,6 +73,17 @@ SM_QUAL double sm_u2d(uint64_t u) {
 SM_QUAL int32_t sm_hi(double x) { return (int32_t)(sm_d2u(x) >> 32); }
 
 SM_QUAL double sm_fma(double a, double b, double c) { return fma(a, b, c); }
+/* A constant the device should keep in a VGPR pair.  gfx950 has no 64-bit
+ * literal operands, so every fp64 constant lives in an SGPR pair; the tick
+ * loop needs more of them than there are SGPRs and the compiler then
+ * re-materialises them (two s_mov_b32 per use) inside the loop.  An empty asm
+ * with a "v" operand moves the value into VGPRs once (the asm is loop
+ * invariant, so it is hoisted); the value itself is unchanged.  Host: identity. */
+#if defined(__HIP_DEVICE_COMPILE__)
+SM_QUAL double sm_vconst(double x) { asm("" : "+v"(x)); return x; }
+#else
+SM_QUAL double sm_vconst(double x) { return x; }
+#endif
 SM_QUAL float sm_fmaf(float a, float b, float c) { return fmaf(a, b, c); }
 
 /* ------------------------------------------------ NumPy/OpenBLAS orders */
@@ -135,9 +146,9 @@ SM_QUAL void sm_np_sincosf(float x, float* s_out, float* c_out) {
 
 /* ------------------------------------------------- fp64 sin/cos (fdlibm) */
 SM_QUAL double sm_ksin(double x, double y, int iy) {
-    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
-                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
-                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    const double S1 = sm_vconst(-1.66666666666666324348e-01), S2 = sm_vconst(8.33333333332248946124e-03),
+                 S3 = sm_vconst(-1.98412698298579493134e-04), S4 = sm_vconst(2.75573137070700676789e-06),
+                 S5 = sm_vconst(-2.50507602534068634195e-08), S6 = sm_vconst(1.58969099521155010221e-10);
     double z = x * x, w = z * z;
     double r = S2 + z * (S3 + z * S4) + z * w * (S5 + z * S6);
     double v = z * x;
@@ -145,9 +156,9 @@ SM_QUAL double sm_ksin(double x, double y, int iy) {
     return x - ((z * (0.5 * y - v * r) - y) - v * S1);
 }
 SM_QUAL double sm_kcos(double x, double y) {
-    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
-                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
-                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    const double C1 = sm_vconst(4.16666666666666019037e-02), C2 = sm_vconst(-1.38888888888741095749e-03),
+                 C3 = sm_vconst(2.48015872894767294178e-05), C4 = sm_vconst(-2.75573143513906633035e-07),
+                 C5 = sm_vconst(2.08757232129817482790e-09), C6 = sm_vconst(-1.13596475577881948265e-11);
     double z = x * x, w = z * z;
     double r = z * (C1 + z * (C2 + z * C3)) + w * w * (C4 + z * (C5 + z * C6));
     double hz = 0.5 * z;
