@@ -34,7 +34,8 @@ static_assert(kBlock == salp::LANES, "LDS cache stride is the workgroup size");
 
 template <bool RAND>
 __device__ __forceinline__ void run_cycle(Hot& h, const Params& P, salp::Cache32 c32) {
-    for (int g = 0; h.ct < h.b2 && g < kMaxTicksPerCycle; ++g) salp::tick<false, RAND>(h, P, c32);
+    const Params PV = salp::pin_params(P);
+    for (int g = 0; h.ct < h.b2 && g < kMaxTicksPerCycle; ++g) salp::tick<false, RAND>(h, PV, c32);
 }
 
 // The loop of Robot.step_through_cycle with record=True (src/robot.py:
