@@ -16,7 +16,10 @@ scan (HIP kernel ``salp_gae``) and the policy all stay in HBM:
   normalisation per minibatch, grad-norm clipping, Adam;
 * multi-GPU: one process per GPU, each with its own env shard; gradients are
   averaged with one flat all-reduce per minibatch (torch.distributed, ``nccl``
-  = RCCL over xGMI; the MLP's gradients are ~20 KB, so one bucket).
+  = RCCL over xGMI; the MLP's gradients are ~20 KB, so one bucket);
+* single GPU: the whole minibatch update (forward, backward, clipping, Adam)
+  is captured once into a HIP graph and replayed per minibatch; the small MLP
+  is otherwise bound by ~60 kernel launches per step.
 
 The policy is SB3's ``MlpPolicy`` for PPO (separate 64-64 tanh actor and critic,
 orthogonal init, state-independent log-std).  The reference's RecurrentPPO
@@ -148,7 +151,8 @@ class PPO:
 
     def __init__(self, policy, env, learning_rate=3e-4, n_steps=2048, batch_size=64, n_epochs=10, gamma=0.99,
                  gae_lambda=0.95, clip_range=0.2, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5,
-                 normalize_advantage=True, seed=0, device=None, verbose=0, reset_nonfinite=True):
+                 normalize_advantage=True, seed=0, device=None, verbose=0, reset_nonfinite=True,
+                 use_graphs=None):
         if policy not in ("MlpPolicy", None) and not isinstance(policy, nn.Module):
             raise ValueError("policy must be 'MlpPolicy' or an nn.Module")
         self.env = env
@@ -164,7 +168,12 @@ class PPO:
         if dist.is_available() and dist.is_initialized():   # identical initial weights on every rank
             for p in self.policy.parameters():
                 dist.broadcast(p.data, 0)
-        self.opt = torch.optim.Adam(self.policy.parameters(), lr=learning_rate, eps=1e-5)
+        multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        self.use_graphs = (not multi) if use_graphs is None else bool(use_graphs) and not multi
+        self.opt = torch.optim.Adam(self.policy.parameters(), lr=learning_rate, eps=1e-5,
+                                    capturable=self.use_graphs)
+        self._graph = None
+        self._graph_warm = 0
         self.n_steps, self.batch_size, self.n_epochs = int(n_steps), int(batch_size), int(n_epochs)
         self.gamma, self.gae_lambda, self.clip_range = gamma, gae_lambda, clip_range
         self.ent_coef, self.vf_coef, self.max_grad_norm = ent_coef, vf_coef, max_grad_norm
@@ -231,40 +240,72 @@ class PPO:
         r.terminated[bad] = True     # terminal: no gamma * V(terminal_obs) bootstrap
 
     # ----------------------------------------------------------- update
-    def train(self):
+    def _minibatch(self, idx, acc):
+        """One SB3 PPO gradient step on rollout rows `idx`; adds
+        (pg_loss, vf_loss, entropy, clip_fraction) to `acc`."""
         b, pol = self.buf, self.policy
         N = self.n_steps * self.n_envs
-        obs = b.obs.reshape(N, -1)
-        act = b.actions.reshape(N, -1)
-        old_lp = b.log_probs.reshape(N)
-        adv_all = b.advantages.reshape(N)
-        ret = b.returns.reshape(N)
-        stats = {"pg_loss": 0.0, "vf_loss": 0.0, "entropy": 0.0, "clip_frac": 0.0, "n": 0}
+        v, lp, ent = pol.evaluate(b.obs.reshape(N, -1)[idx], b.actions.reshape(N, -1)[idx])
+        adv = b.advantages.reshape(N)[idx]
+        if self.normalize_advantage and idx.numel() > 1:
+            adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+        ratio = torch.exp(lp - b.log_probs.reshape(N)[idx])
+        pg = -torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - self.clip_range, 1 + self.clip_range)).mean()
+        vf = torch.nn.functional.mse_loss(b.returns.reshape(N)[idx], v)
+        ent_loss = -ent.mean()
+        loss = pg + self.ent_coef * ent_loss + self.vf_coef * vf
+        loss.backward()
+        allreduce_gradients(list(pol.parameters()))
+        nn.utils.clip_grad_norm_(pol.parameters(), self.max_grad_norm)
+        self.opt.step()
+        clip = ((ratio - 1).abs() > self.clip_range).float().mean()
+        acc += torch.stack([pg.detach(), vf.detach(), -ent_loss.detach(), clip.detach()])
+
+    def _graphed_minibatch(self, idx):
+        """The same step through a HIP graph: three eager warm-up steps on a
+        side stream, then one capture, then replays (static index / stats
+        buffers; Adam is capturable)."""
+        if self._graph is None:
+            if self._graph_warm == 0:
+                self._g_idx = torch.empty_like(idx)
+                self._g_acc = torch.zeros(4, device=self.device)
+            self._g_idx.copy_(idx)
+            if self._graph_warm < 3:
+                side = torch.cuda.Stream(self.device)
+                side.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(side):
+                    self.opt.zero_grad(set_to_none=True)
+                    self._minibatch(self._g_idx, self._g_acc)
+                torch.cuda.current_stream(self.device).wait_stream(side)
+                self._graph_warm += 1
+                return
+            self.opt.zero_grad(set_to_none=True)
+            self._graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._graph):
+                self._minibatch(self._g_idx, self._g_acc)
+        else:
+            self._g_idx.copy_(idx)
+        self._graph.replay()
+
+    def train(self):
+        N = self.n_steps * self.n_envs
+        acc = torch.zeros(4, device=self.device)
+        steps = 0
         for _ in range(self.n_epochs):
             perm = torch.randperm(N, generator=self.gen).to(self.device)
             for s in range(0, N, self.batch_size):
                 idx = perm[s:s + self.batch_size]
-                v, lp, ent = pol.evaluate(obs[idx], act[idx])
-                adv = adv_all[idx]
-                if self.normalize_advantage and len(idx) > 1:
-                    adv = (adv - adv.mean()) / (adv.std() + 1e-8)
-                ratio = torch.exp(lp - old_lp[idx])
-                pg = -torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - self.clip_range, 1 + self.clip_range)).mean()
-                vf = torch.nn.functional.mse_loss(ret[idx], v)
-                ent_loss = -ent.mean()
-                loss = pg + self.ent_coef * ent_loss + self.vf_coef * vf
-                self.opt.zero_grad(set_to_none=False)
-                loss.backward()
-                allreduce_gradients(list(pol.parameters()))
-                nn.utils.clip_grad_norm_(pol.parameters(), self.max_grad_norm)
-                self.opt.step()
-                stats["pg_loss"] += pg.detach()
-                stats["vf_loss"] += vf.detach()
-                stats["entropy"] += -ent_loss.detach()
-                stats["clip_frac"] += ((ratio - 1).abs() > self.clip_range).float().mean().detach()
-                stats["n"] += 1
-        n = max(stats.pop("n"), 1)
-        return {k: float(v) / n for k, v in stats.items()}
+                if self.use_graphs and idx.numel() == self.batch_size:
+                    self._graphed_minibatch(idx)
+                else:
+                    self.opt.zero_grad(set_to_none=False)
+                    self._minibatch(idx, acc)
+                steps += 1
+        if self.use_graphs and self._graph_warm > 0:
+            acc = acc + self._g_acc
+            self._g_acc.zero_()
+        vals = (acc / max(steps, 1)).tolist()
+        return dict(zip(("pg_loss", "vf_loss", "entropy", "clip_frac"), vals))
 
     def learn(self, total_timesteps, log_interval=1):
         it = 0
