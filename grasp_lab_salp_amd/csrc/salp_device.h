@@ -68,6 +68,7 @@ struct Params {
     double angle_speed;      /* 31*pi/30 */
     double obstacle_radius, x_min, x_max, y_min, y_max, sep;
     double init_angle1, init_angle2;
+    SmPoly sk;               /* sin/cos kernel coefficients (pinned with the rest) */
     int32_t num_obstacles, max_cycles, obs_dim;
     /* randomisation switches (SalpParams; salp_random.h) */
     int32_t rand_dyn, rand_dist, rand_act, rand_obs, latency;
@@ -76,14 +77,20 @@ struct Params {
     uint64_t seed;
 };
 
-/* The launch constants the tick reads, moved into VGPRs for the tick loop
- * (see sm_vconst: the kernel arguments otherwise hold SGPRs the loop needs
- * for its fp64 constants).  Values unchanged. */
+/* The launch constants the tick reads, moved into VGPRs for the tick loop.
+ * gfx950 has no 64-bit literal operands, so every fp64 constant otherwise lives
+ * in an SGPR pair; the tick loop needs more of them than there are SGPRs and
+ * the compiler then re-materialises them (two s_mov_b32 per use) inside the
+ * loop.  The empty asm makes each value opaque once, before the loop, so it
+ * stays in its VGPR pair.  Values unchanged. */
 SD Params pin_params(const Params& P) {
     Params v = P;
     asm volatile("" : "+v"(v.L0), "+v"(v.W0), "+v"(v.dry_mass), "+v"(v.nozzle_mass), "+v"(v.density),
                  "+v"(v.nozzle_area), "+v"(v.mid_x), "+v"(v.tube_volume), "+v"(v.net_tube_mass),
                  "+v"(v.com_mass_sum), "+v"(v.P1000tv), "+v"(v.end_aspect), "+v"(v.aspect_den));
+    asm volatile("" : "+v"(v.sk.S1), "+v"(v.sk.S2), "+v"(v.sk.S3), "+v"(v.sk.S4), "+v"(v.sk.S5),
+                 "+v"(v.sk.S6), "+v"(v.sk.C1), "+v"(v.sk.C2), "+v"(v.sk.C3), "+v"(v.sk.C4), "+v"(v.sk.C5),
+                 "+v"(v.sk.C6));
     return v;
 }
 
@@ -632,9 +639,9 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     }
     {   /* to_world_frame_jit (src/dynamics.py:34-58) at the new angles */
         double ss, cs;
-        sm_sincos(h.e0, &h.sp, &h.cp);
-        sm_sincos(h.e1, &h.st, &h.cth);
-        sm_sincos(h.e2, &ss, &cs);
+        sm_sincos_p(h.e0, &h.sp, &h.cp, P.sk);
+        sm_sincos_p(h.e1, &h.st, &h.cth, P.sk);
+        sm_sincos_p(h.e2, &ss, &cs, P.sk);
         Rot R = rot_sc(h.sp, h.cp, h.st, h.cth, ss, cs);
         double vw[3];
         rot_apply(R, h.v0, h.v1, h.v2, vw);

@@ -203,7 +203,7 @@ __device__ __forceinline__ void rollout_boundary(Hot& h, ST S, const Params& P, 
 // All launch arguments in one struct: the env-step epilogue re-reads them from
 // the kernarg segment (scalar loads) where it runs, so that nothing it needs
 // is held in SGPRs across the tick loop — which then compiles exactly like a
-// standalone tick loop (its polynomial constants stay resident in SGPRs).
+// standalone tick loop (its fp64 constants pinned in VGPRs, pin_params).
 struct RolloutArgs {
     double* S;
     Params P;
@@ -346,7 +346,8 @@ __global__ __launch_bounds__(kBlock) void k_tick_bench(double* S, Params P, int3
     salp::load_hot(h, S, P, i);
     salp::resume_cycle(h, S, P, i);
     salp::fill_cache32(P, h.c, c32);
-    for (int32_t k = 0; k < n_ticks; ++k) salp::tick<false, false>(h, P, c32);
+    const Params PV = salp::pin_params(P);
+    for (int32_t k = 0; k < n_ticks; ++k) salp::tick<false, false>(h, PV, c32);
     salp::store_hot(h, S, P, i);
 }
 
@@ -424,6 +425,7 @@ Params derive(const SalpParams& p, int64_t n, uint64_t seed, int64_t offset) {
     Params d{};
     const double PI = salp::PI;
     d.L0 = p.init_length; d.W0 = p.init_width; d.maxc = p.max_contraction;
+    d.sk = sm_poly();
     d.dry_mass = p.dry_mass; d.nozzle_mass = p.nozzle_mass; d.density = p.density;
     d.nozzle_area = p.nozzle_area;
     d.mid_x = -(p.nozzle_length1 + p.nozzle_length2);

@@ -73,17 +73,6 @@ SM_QUAL double sm_u2d(uint64_t u) {
 SM_QUAL int32_t sm_hi(double x) { return (int32_t)(sm_d2u(x) >> 32); }
 
 SM_QUAL double sm_fma(double a, double b, double c) { return fma(a, b, c); }
-/* A constant the device should keep in a VGPR pair.  gfx950 has no 64-bit
- * literal operands, so every fp64 constant lives in an SGPR pair; the tick
- * loop needs more of them than there are SGPRs and the compiler then
- * re-materialises them (two s_mov_b32 per use) inside the loop.  An empty asm
- * with a "v" operand moves the value into VGPRs once (the asm is loop
- * invariant, so it is hoisted); the value itself is unchanged.  Host: identity. */
-#if defined(__HIP_DEVICE_COMPILE__)
-SM_QUAL double sm_vconst(double x) { asm("" : "+v"(x)); return x; }
-#else
-SM_QUAL double sm_vconst(double x) { return x; }
-#endif
 SM_QUAL float sm_fmaf(float a, float b, float c) { return fmaf(a, b, c); }
 
 /* ------------------------------------------------ NumPy/OpenBLAS orders */
@@ -145,26 +134,36 @@ SM_QUAL void sm_np_sincosf(float x, float* s_out, float* c_out) {
 }
 
 /* ------------------------------------------------- fp64 sin/cos (fdlibm) */
-SM_QUAL double sm_ksin(double x, double y, int iy) {
-    const double S1 = sm_vconst(-1.66666666666666324348e-01), S2 = sm_vconst(8.33333333332248946124e-03),
-                 S3 = sm_vconst(-1.98412698298579493134e-04), S4 = sm_vconst(2.75573137070700676789e-06),
-                 S5 = sm_vconst(-2.50507602534068634195e-08), S6 = sm_vconst(1.58969099521155010221e-10);
-    double z = x * x, w = z * z;
-    double r = S2 + z * (S3 + z * S4) + z * w * (S5 + z * S6);
-    double v = z * x;
-    if (iy == 0) return x + v * (S1 + z * r);
-    return x - ((z * (0.5 * y - v * r) - y) - v * S1);
+/* The kernel polynomials' coefficients (fdlibm __kernel_sin / __kernel_cos).
+ * Passed by value so that a hot loop can hand in a copy kept in VGPRs
+ * (salp_device.h pin_params): gfx950 has no 64-bit literal operands, and
+ * pinning each use separately costs a v_mov_b64 per coefficient per call. */
+typedef struct {
+    double S1, S2, S3, S4, S5, S6, C1, C2, C3, C4, C5, C6;
+} SmPoly;
+SM_QUAL SmPoly sm_poly(void) {
+    SmPoly k = {-1.66666666666666324348e-01, 8.33333333332248946124e-03, -1.98412698298579493134e-04,
+                2.75573137070700676789e-06,  -2.50507602534068634195e-08, 1.58969099521155010221e-10,
+                4.16666666666666019037e-02,  -1.38888888888741095749e-03, 2.48015872894767294178e-05,
+                -2.75573143513906633035e-07, 2.08757232129817482790e-09,  -1.13596475577881948265e-11};
+    return k;
 }
-SM_QUAL double sm_kcos(double x, double y) {
-    const double C1 = sm_vconst(4.16666666666666019037e-02), C2 = sm_vconst(-1.38888888888741095749e-03),
-                 C3 = sm_vconst(2.48015872894767294178e-05), C4 = sm_vconst(-2.75573143513906633035e-07),
-                 C5 = sm_vconst(2.08757232129817482790e-09), C6 = sm_vconst(-1.13596475577881948265e-11);
+SM_QUAL double sm_ksin_p(double x, double y, int iy, SmPoly K) {
     double z = x * x, w = z * z;
-    double r = z * (C1 + z * (C2 + z * C3)) + w * w * (C4 + z * (C5 + z * C6));
+    double r = K.S2 + z * (K.S3 + z * K.S4) + z * w * (K.S5 + z * K.S6);
+    double v = z * x;
+    if (iy == 0) return x + v * (K.S1 + z * r);
+    return x - ((z * (0.5 * y - v * r) - y) - v * K.S1);
+}
+SM_QUAL double sm_kcos_p(double x, double y, SmPoly K) {
+    double z = x * x, w = z * z;
+    double r = z * (K.C1 + z * (K.C2 + z * K.C3)) + w * w * (K.C4 + z * (K.C5 + z * K.C6));
     double hz = 0.5 * z;
     w = 1.0 - hz;
     return w + (((1.0 - w) - hz) + (z * r - x * y));
 }
+SM_QUAL double sm_ksin(double x, double y, int iy) { return sm_ksin_p(x, y, iy, sm_poly()); }
+SM_QUAL double sm_kcos(double x, double y) { return sm_kcos_p(x, y, sm_poly()); }
 /* Cody-Waite reduction for |x| < 2^20*pi/2 (fdlibm __ieee754_rem_pio2,
  * medium case).  Returns n with x = n*pi/2 + (y0 + y1). */
 SM_QUAL int sm_rem_pio2(double x, double* y0, double* y1) {
@@ -197,16 +196,16 @@ SM_QUAL int sm_rem_pio2(double x, double* y0, double* y1) {
     *y1 = (r - y) - w;
     return (int)fn;
 }
-SM_QUAL void sm_sincos(double x, double* s_out, double* c_out) {
+SM_QUAL void sm_sincos_p(double x, double* s_out, double* c_out, SmPoly K) {
     int32_t ix = sm_hi(x) & 0x7fffffff;
     if (ix <= 0x3fe921fb) { /* |x| <= pi/4 */
-        *s_out = sm_ksin(x, 0.0, 0);
-        *c_out = sm_kcos(x, 0.0);
+        *s_out = sm_ksin_p(x, 0.0, 0, K);
+        *c_out = sm_kcos_p(x, 0.0, K);
         return;
     }
     double y0, y1;
     int n = sm_rem_pio2(x, &y0, &y1);
-    double s = sm_ksin(y0, y1, 1), c = sm_kcos(y0, y1);
+    double s = sm_ksin_p(y0, y1, 1, K), c = sm_kcos_p(y0, y1, K);
     switch (n & 3) {
         case 0: *s_out = s; *c_out = c; break;
         case 1: *s_out = c; *c_out = -s; break;
@@ -214,6 +213,7 @@ SM_QUAL void sm_sincos(double x, double* s_out, double* c_out) {
         default: *s_out = -c; *c_out = s; break;
     }
 }
+SM_QUAL void sm_sincos(double x, double* s_out, double* c_out) { sm_sincos_p(x, s_out, c_out, sm_poly()); }
 SM_QUAL double sm_sin(double x) { double s, c; sm_sincos(x, &s, &c); return s; }
 SM_QUAL double sm_cos(double x) { double s, c; sm_sincos(x, &s, &c); return c; }
 SM_QUAL double sm_tan(double x) { double s, c; sm_sincos(x, &s, &c); return s / c; }
