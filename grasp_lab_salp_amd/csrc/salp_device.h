@@ -641,7 +641,7 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
         double ss, cs;
         sm_sincos_p(h.e0, &h.sp, &h.cp, P.sk);
         sm_sincos_p(h.e1, &h.st, &h.cth, P.sk);
-        sm_sincos_p(h.e2, &ss, &cs, P.sk);
+        sm_sincos_nb_p(h.e2, &ss, &cs, P.sk);   /* yaw: both kinds of argument in a wave */
         Rot R = rot_sc(h.sp, h.cp, h.st, h.cth, ss, cs);
         double vw[3];
         rot_apply(R, h.v0, h.v1, h.v2, vw);

@@ -365,6 +365,10 @@ __global__ void k_math_selftest(const double* x, const double* y, int64_t n, dou
     sm_np_sincosf((float)x[i], &s, &c);
     out[7 * n + i] = c;
     out[8 * n + i] = s;
+    double snb, cnb;
+    sm_sincos_nb_p(x[i], &snb, &cnb, sm_poly());
+    out[9 * n + i] = snb;
+    out[10 * n + i] = cnb;
 }
 
 const char* const kFieldNames[SALP_NUM_FIELDS] = {

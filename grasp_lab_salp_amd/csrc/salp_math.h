@@ -213,6 +213,27 @@ SM_QUAL void sm_sincos_p(double x, double* s_out, double* c_out, SmPoly K) {
         default: *s_out = -c; *c_out = s; break;
     }
 }
+/* sm_sincos_p without the |x| <= pi/4 branch: every lane runs the reduction,
+ * lanes below pi/4 then take (x, 0, quadrant 0) and the iy == 0 form of the sin
+ * kernel (the cos kernel with y = 0 is that form already: x * 0 is exact).
+ * Bit-identical to sm_sincos_p; cheaper where a wave holds both kinds of
+ * argument (the yaw, uniform over the circle), since the branchy version then
+ * runs both paths. */
+SM_QUAL void sm_sincos_nb_p(double x, double* s_out, double* c_out, SmPoly K) {
+    const int small = (sm_hi(x) & 0x7fffffff) <= 0x3fe921fb;
+    double y0, y1;
+    int n = sm_rem_pio2(x, &y0, &y1);
+    if (small) { y0 = x; y1 = 0.0; n = 0; }
+    const double z = y0 * y0, w = z * z;
+    const double r = K.S2 + z * (K.S3 + z * K.S4) + z * w * (K.S5 + z * K.S6);
+    const double v = z * y0;
+    const double s = small ? y0 + v * (K.S1 + z * r) : y0 - ((z * (0.5 * y1 - v * r) - y1) - v * K.S1);
+    const double c = sm_kcos_p(y0, y1, K);
+    const int q = n & 3;
+    const double a = (q & 1) ? c : s, b = (q & 1) ? s : c;
+    *s_out = (q & 2) ? -a : a;
+    *c_out = ((q + 1) & 2) ? -b : b;
+}
 SM_QUAL void sm_sincos(double x, double* s_out, double* c_out) { sm_sincos_p(x, s_out, c_out, sm_poly()); }
 SM_QUAL double sm_sin(double x) { double s, c; sm_sincos(x, &s, &c); return s; }
 SM_QUAL double sm_cos(double x) { double s, c; sm_sincos(x, &s, &c); return c; }

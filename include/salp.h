@@ -225,8 +225,8 @@ int salp_bench_ticks(SalpEnv* h, int32_t n_ticks, void* stream);
 /* Device address of the handle's state buffer (zero-copy views). */
 int64_t salp_state_ptr(SalpEnv* h);
 /* Device-side self-test of salp_math.h: out[i] = f(x[i]) for f in
- * {sin, cos, tan, atan2(x, y), asin, acos, cube, np_cosf, np_sinf}.
- * x, y [n]; out [9][n]. */
+ * {sin, cos, tan, atan2(x, y), asin, acos, cube, np_cosf, np_sinf, sin and cos
+ * of the branch-free sincos}.  x, y [n]; out [11][n]. */
 int salp_math_selftest(const double* x, const double* y, int64_t n, double* out, void* stream);
 
 /* State fields.  Names follow the reference attribute they hold. */

@@ -19,8 +19,15 @@ LIB_PATH = os.path.join(HERE, "libsalp_oracle.so")
 _lib = None
 
 
+SOURCES = [os.path.join(HERE, "salp_oracle.c"), os.path.join(HERE, "..", "include", "salp.h")] + [
+    os.path.join(HERE, "..", "grasp_lab_salp_amd", "csrc", f) for f in ("salp_math.h", "salp_philox.h",
+                                                                          "salp_random.h")]
+
+
 def build(force=False):
-    if force or not os.path.exists(LIB_PATH):
+    stale = not os.path.exists(LIB_PATH) or any(
+        os.path.getmtime(s) > os.path.getmtime(LIB_PATH) for s in SOURCES)
+    if force or stale:
         subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB_PATH
 
@@ -198,7 +205,7 @@ def robot_trace(actions, params=None, max_rows=200000):
 def math_selftest(x, y):
     x = np.ascontiguousarray(x, np.float64)
     y = np.ascontiguousarray(y, np.float64)
-    out = np.zeros((9, len(x)), np.float64)
+    out = np.zeros((11, len(x)), np.float64)
     lib().oracle_math_selftest(_p(x, ctypes.c_double), _p(y, ctypes.c_double), len(x),
                                _p(out, ctypes.c_double))
     return out

@@ -51,13 +51,13 @@ def test_device_math_equals_oracle_math():
     L = _lib.load()
     xd = torch.tensor(x, device="cuda")
     yd = torch.tensor(y, device="cuda")
-    out = torch.empty((9, len(x)), dtype=torch.float64, device="cuda")
+    out = torch.empty((11, len(x)), dtype=torch.float64, device="cuda")
     _lib.check(L.salp_math_selftest(ctypes.c_void_p(xd.data_ptr()), ctypes.c_void_p(yd.data_ptr()),
                                     len(x), ctypes.c_void_p(out.data_ptr()), None))
     torch.cuda.synchronize()
     ref = orc.math_selftest(x, y)
     g = _cpu(out)
-    for r in range(9):
+    for r in range(11):
         assert np.array_equal(g[r], ref[r], equal_nan=True), f"math row {r}: {np.sum(g[r] != ref[r])} mismatches"
 
 

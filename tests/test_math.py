@@ -84,3 +84,19 @@ def test_philox_known_answers():
                                                                  0x6d5451fd]
     assert oracle.philox([0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344], [0xa4093822, 0x299f31d0]) == \
         [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]
+
+
+def test_branch_free_sincos_equals_sincos():
+    """sm_sincos_nb_p (every lane reduced, variant picked per lane) is
+    bit-identical to sm_sincos, around the pi/4 switch, the quadrant edges,
+    signed zeros and non-finite inputs included."""
+    rng = np.random.default_rng(5)
+    q = np.pi / 4
+    edges = np.concatenate([[np.nextafter(q, 0), q, np.nextafter(q, 4)], np.arange(-8, 9) * (np.pi / 4)])
+    x = np.concatenate([rng.uniform(-np.pi, np.pi, 200000), rng.uniform(-1e3, 1e3, 20000),
+                        rng.uniform(-1e-6, 1e-6, 2000), edges, -edges,
+                        [0.0, -0.0, np.inf, -np.inf, np.nan, 5e-324, -5e-324, 1e-300]])
+    out = oracle.math_selftest(x, np.zeros(len(x)))
+    for r_nb, r in ((9, 0), (10, 1)):
+        assert np.array_equal(out[r_nb], out[r], equal_nan=True)
+        assert np.array_equal(np.signbit(out[r_nb]), np.signbit(out[r]))
