@@ -107,6 +107,29 @@ SD double div_dt(double x) {
     const double q = sm_fma(sm_fma(-DT, q0, x), 100.0, q0);
     return __builtin_amdgcn_div_fixup(q, DT, x);
 }
+/* x / d with the divisor's reciprocal shared between quotients.  The
+ * compiler's f64 division is: v_div_scale of both operands (the identity
+ * unless an operand lies near the exponent limits), v_rcp_f64 and two Newton
+ * steps (a function of d alone), q0 = x * r, one FMA remainder correction
+ * (v_div_fmas: an FMA when nothing was scaled) and v_div_fixup.  Rcp is the
+ * refined reciprocal, computed once per divisor; qdiv is the per-quotient
+ * tail, 4 instructions instead of 10 and no VCC hazard.  Equal to x / d bit
+ * for bit unless v_div_scale would rescale (|x| within 2^53 of the double
+ * range limits or of the denormals): the masses, inertias, cosines, lengths
+ * and constants the tick divides by are far from both (math selftest row 11
+ * checks it against the oracle's C division). */
+struct Rcp { double d, r; };
+SD Rcp rcp_of(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    r = sm_fma(r, sm_fma(-d, r, 1.0), r);
+    r = sm_fma(r, sm_fma(-d, r, 1.0), r);
+    return Rcp{d, r};
+}
+SD double qdiv(double x, Rcp k) {
+    const double q0 = x * k.r;
+    const double q = sm_fma(sm_fma(-k.d, q0, x), k.r, q0);
+    return __builtin_amdgcn_div_fixup(q, k.d, x);
+}
 SD float sqf(float x) { return (float)((double)x * (double)x); }
 SD float cubef(float x) {
     double p = (double)x * (double)x;
@@ -208,10 +231,10 @@ SD double center_of_mass(const Params& P, const Core& c, double wm, bool f) {
     double pnx = r32(r32(-c.lh - sel(f, 0.025), f) + sel(f, 0.05), f);
     double num = c.wme * 0.0 - P.P1000tv * ptx;
     double den = r32(c.wme - sel(f, P.P1000tv), f);
-    double pwx = num / den;
+    double pwx = qdiv(num, rcp_of(den));
     double total = r32(sel(f, P.com_mass_sum) + wm, f);
-    return (TUBE_MASS * ptx + P.nozzle_mass * pnx + BUOY_MASS * pbx + SKIN_MASS * 0.0 + wm * pwx) /
-           total;
+    return qdiv(TUBE_MASS * ptx + P.nozzle_mass * pnx + BUOY_MASS * pbx + SKIN_MASS * 0.0 + wm * pwx,
+                rcp_of(total));
 }
 
 /* Everything the next tick's dynamics needs from (length, width, volume,
@@ -234,8 +257,8 @@ SD Shape shape_of(const Params& P, const Core& c, double L, double W, bool f) {
     double pi = sel(f, PI);
     s.A0 = r32(r32(pi * c.wh, f) * c.wh, f);
     s.A1 = r32(r32(pi * c.lh, f) * c.wh, f);
-    double aspect = r32(L / W, f);
-    double nr = r32(r32(aspect - sel(f, P.end_aspect), f) / sel(f, P.aspect_den), f);
+    double aspect = r32(qdiv(L, rcp_of(W)), f);
+    double nr = r32(qdiv(r32(aspect - sel(f, P.end_aspect), f), rcp_of(sel(f, P.aspect_den))), f);
     nr = nr < 0.0 ? 0.0 : nr;
     s.nr = nr > 1.0 ? 1.0 : nr;
     return s;
@@ -286,7 +309,7 @@ SD void jet_rates(const Params& P, double V, double pV, double wm, bool g32, boo
         g.speed = r32(r32(r32(V - pV, true) / sel(true, DT), true) / sel(true, P.nozzle_area), true);
     } else {
         g.mr = div_dt(wm - pwm);
-        g.speed = div_dt(V - pV) / P.nozzle_area;
+        g.speed = qdiv(div_dt(V - pV), rcp_of(P.nozzle_area));
     }
 }
 SD Geo make_geo(const Params& P, const Core& c, double L, double W, double V, double pV, bool g32,
@@ -558,14 +581,15 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     double ff0 = acc_x * m, ff1 = acc_y * m, ff2 = acc_z * m;
     /* total force and linear acceleration (src/dynamics.py:5-10) */
     double na0, na1, na2;
+    const Rcp rm = rcp_of(m);
     if (RAND) {   /* + force noise (z: zero) */
-        na0 = (((((jf0 + df0) + af0) + cf0) + nf0) + ff0) / m;
-        na1 = (((((jf1 + df1) + af1) + cf1) + nf1) + ff1) / m;
-        na2 = (((((jf2 + df2) + af2) + cf2) + 0.0) + ff2) / m;
+        na0 = qdiv(((((jf0 + df0) + af0) + cf0) + nf0) + ff0, rm);
+        na1 = qdiv(((((jf1 + df1) + af1) + cf1) + nf1) + ff1, rm);
+        na2 = qdiv(((((jf2 + df2) + af2) + cf2) + 0.0) + ff2, rm);
     } else {
-        na0 = ((((jf0 + df0) + af0) + cf0) + ff0) / m;
-        na1 = ((((jf1 + df1) + af1) + cf1) + ff1) / m;
-        na2 = ((((jf2 + df2) + af2) + cf2) + ff2) / m;
+        na0 = qdiv((((jf0 + df0) + af0) + cf0) + ff0, rm);
+        na1 = qdiv((((jf1 + df1) + af1) + cf1) + ff1, rm);
+        na2 = qdiv((((jf2 + df2) + af2) + cf2) + ff2, rm);
     }
     /* ---------------- Euler ---------------- */
     const double I0 = g.I0, I1 = g.I1;
@@ -594,14 +618,15 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     double amt2 = -((at2 * h.al2 + (h.w0 * atw1 - h.w1 * atw0)) + (h.v0 * amv1 - h.v1 * amv0));
     /* total torque and angular acceleration (src/dynamics.py:13-17) */
     double nal0, nal1, nal2;
+    const Rcp rI0 = rcp_of(I0), rI1 = rcp_of(I1);
     if (RAND) {   /* + torque noise (x, y: zero) */
-        nal0 = ((((dt0 + ct0) + dft0) + amt0) + 0.0) / I0;
-        nal1 = (((((jt1 + dt1) + ct1) + dft1) + amt1) + 0.0) / I1;
-        nal2 = (((((jt2 + dt2) + ct2) + dft2) + amt2) + nt2) / I1;
+        nal0 = qdiv((((dt0 + ct0) + dft0) + amt0) + 0.0, rI0);
+        nal1 = qdiv(((((jt1 + dt1) + ct1) + dft1) + amt1) + 0.0, rI1);
+        nal2 = qdiv(((((jt2 + dt2) + ct2) + dft2) + amt2) + nt2, rI1);
     } else {
-        nal0 = (((dt0 + ct0) + dft0) + amt0) / I0;
-        nal1 = ((((jt1 + dt1) + ct1) + dft1) + amt1) / I1;
-        nal2 = ((((jt2 + dt2) + ct2) + dft2) + amt2) / I1;
+        nal0 = qdiv(((dt0 + ct0) + dft0) + amt0, rI0);
+        nal1 = qdiv((((jt1 + dt1) + ct1) + dft1) + amt1, rI1);
+        nal2 = qdiv((((jt2 + dt2) + ct2) + dft2) + amt2, rI1);
     }
     if (REC) {
         const double z = 0.0;
@@ -626,10 +651,11 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     h.v0 = h.v0 + na0 * DT; h.v1 = h.v1 + na1 * DT; h.v2 = h.v2 + na2 * DT;
     h.w0 = h.w0 + nal0 * DT; h.w1 = h.w1 + nal1 * DT; h.w2 = h.w2 + nal2 * DT;
     {   /* to_euler_angle_rate_jit (src/dynamics.py:20-31) at the current angles */
-        double tt = h.st / h.cth;
+        const Rcp rc = rcp_of(h.cth);
+        double tt = qdiv(h.st, rc);
         double r0 = sm_fma(h.cp * tt, h.w2, h.w0 + (h.sp * tt) * h.w1);
         double r1 = sm_fma(-h.sp, h.w2, h.cp * h.w1);
-        double r2 = sm_fma(h.cp / h.cth, h.w2, (h.sp / h.cth) * h.w1);
+        double r2 = sm_fma(qdiv(h.cp, rc), h.w2, qdiv(h.sp, rc) * h.w1);
         h.e0 = h.e0 + r0 * DT; h.e1 = h.e1 + r1 * DT; h.e2 = h.e2 + r2 * DT;
         if (REC) {
             rec[(int64_t)SALP_T_ETAR0 * rs] = r0;

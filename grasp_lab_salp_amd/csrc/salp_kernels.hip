@@ -369,6 +369,7 @@ __global__ void k_math_selftest(const double* x, const double* y, int64_t n, dou
     sm_sincos_nb_p(x[i], &snb, &cnb, sm_poly());
     out[9 * n + i] = snb;
     out[10 * n + i] = cnb;
+    out[11 * n + i] = salp::qdiv(x[i], salp::rcp_of(y[i]));   /* the tick's shared-reciprocal division */
 }
 
 const char* const kFieldNames[SALP_NUM_FIELDS] = {

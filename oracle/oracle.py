@@ -205,7 +205,7 @@ def robot_trace(actions, params=None, max_rows=200000):
 def math_selftest(x, y):
     x = np.ascontiguousarray(x, np.float64)
     y = np.ascontiguousarray(y, np.float64)
-    out = np.zeros((11, len(x)), np.float64)
+    out = np.zeros((12, len(x)), np.float64)
     lib().oracle_math_selftest(_p(x, ctypes.c_double), _p(y, ctypes.c_double), len(x),
                                _p(out, ctypes.c_double))
     return out

@@ -1477,6 +1477,7 @@ void oracle_math_selftest(const double* x, const double* y, int64_t n, double* o
         sm_sincos_nb_p(x[i], &snb, &cnb, sm_poly());
         out[9 * n + i] = snb;
         out[10 * n + i] = cnb;
+        out[11 * n + i] = x[i] / y[i];   /* device: qdiv(x, rcp_of(y)) */
     }
 }
 

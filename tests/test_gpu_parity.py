@@ -51,15 +51,42 @@ def test_device_math_equals_oracle_math():
     L = _lib.load()
     xd = torch.tensor(x, device="cuda")
     yd = torch.tensor(y, device="cuda")
-    out = torch.empty((11, len(x)), dtype=torch.float64, device="cuda")
+    out = torch.empty((12, len(x)), dtype=torch.float64, device="cuda")
     _lib.check(L.salp_math_selftest(ctypes.c_void_p(xd.data_ptr()), ctypes.c_void_p(yd.data_ptr()),
                                     len(x), ctypes.c_void_p(out.data_ptr()), None))
     torch.cuda.synchronize()
     ref = orc.math_selftest(x, y)
     g = _cpu(out)
-    for r in range(11):
+    for r in range(12):
         assert np.array_equal(g[r], ref[r], equal_nan=True), f"math row {r}: {np.sum(g[r] != ref[r])} mismatches"
 
+
+
+def test_shared_reciprocal_division_equals_ieee_division():
+    """qdiv(x, rcp_of(y)) (the tick's divisions by mass, inertia, cos(pitch),
+    width, ...) against the oracle's C `x / y` over 200 decades of magnitude,
+    both signs, and the zero / inf operands v_div_fixup handles."""
+    rng = np.random.default_rng(5)
+    n = 200000
+    x = 10.0 ** rng.uniform(-100, 100, n) * rng.choice([-1.0, 1.0], n)
+    y = 10.0 ** rng.uniform(-100, 100, n) * rng.choice([-1.0, 1.0], n)
+    sx = np.array([0.0, -0.0, 5.0, -5.0, np.inf, 2.0, 0.0, 3.0, 1.0, 7.0])
+    sy = np.array([5.0, 5.0, 0.0, -0.0, 2.0, np.inf, 0.0, 3.0, 3.0, 0.1])
+    x, y = np.concatenate([x, sx]), np.concatenate([y, sy])
+    from grasp_lab_salp_amd import _lib
+    import ctypes
+    L = _lib.load()
+    xd = torch.tensor(x, device="cuda")
+    yd = torch.tensor(y, device="cuda")
+    out = torch.empty((12, len(x)), dtype=torch.float64, device="cuda")
+    _lib.check(L.salp_math_selftest(ctypes.c_void_p(xd.data_ptr()), ctypes.c_void_p(yd.data_ptr()),
+                                    len(x), ctypes.c_void_p(out.data_ptr()), None))
+    torch.cuda.synchronize()
+    got = _cpu(out)[11]
+    want = x / y
+    both_nan = np.isnan(got) & np.isnan(want)   # 0/0: NaN payloads differ by platform
+    bad = (got.view(np.uint64) != want.view(np.uint64)) & ~both_nan
+    assert not bad.any(), f"{bad.sum()} quotients differ, e.g. {x[bad][:3]} / {y[bad][:3]}"
 
 def test_fresh_envs_equal_oracle():
     env, o = make_pair(1000)
