@@ -304,13 +304,16 @@ SD Geo make_geo_shape(const Params& P, const Core& c, double L, double W, double
 SD void jet_rates(const Params& P, double V, double pV, double wm, bool g32, bool pv32, Geo& g) {
     const bool b32 = g32 && pv32;
     double pwm = r32(sel(pv32, P.density) * pV, pv32);
-    if (b32) {
-        g.mr = r32(r32(wm - pwm, true) / sel(true, DT), true);
-        g.speed = r32(r32(r32(V - pV, true) / sel(true, DT), true) / sel(true, P.nozzle_area), true);
-    } else {
-        g.mr = div_dt(wm - pwm);
-        g.speed = qdiv(div_dt(V - pV), rcp_of(P.nozzle_area));
-    }
+    /* Both dtypes without a branch.  A float32 quotient is the float64
+     * quotient of the float32 operands rounded to float32 (double rounding is
+     * exact here: 53 >= 2*24 + 2), so it shares the float64 reciprocals. */
+    const Rcp rdt32 = rcp_of(sel(true, DT)), ra32 = rcp_of(sel(true, P.nozzle_area));
+    const double mr32 = r32(qdiv(r32(wm - pwm, true), rdt32), true);
+    const double sp32 = r32(qdiv(r32(qdiv(r32(V - pV, true), rdt32), true), ra32), true);
+    const double mr64 = div_dt(wm - pwm);
+    const double sp64 = qdiv(div_dt(V - pV), rcp_of(P.nozzle_area));
+    g.mr = b32 ? mr32 : mr64;
+    g.speed = b32 ? sp32 : sp64;
 }
 SD Geo make_geo(const Params& P, const Core& c, double L, double W, double V, double pV, bool g32,
                 bool pv32, double wm) {
@@ -356,8 +359,12 @@ SD void body_lw(const Params& P, int phase, double ct, double refill, double mx,
     const double Lc = c32 ? (double)((float)P.L0 - (float)c) : P.L0 - c;
     const double Wc = c32 ? (double)((float)P.W0 + (float)c) : P.W0 + c;
     const double x = (ct - mx) * rr;
-    *L = fill ? (early ? P.L0 - ct * cr : Lc) : (jet ? Lc + x : P.L0);
-    *W = fill ? (early ? P.W0 + ct * cr : Wc) : (jet ? Wc - x : P.W0);
+    /* every arm computed, then flat selects (no branches in the tick) */
+    const double Le = P.L0 - ct * cr, We = P.W0 + ct * cr, Lj = Lc + x, Wj = Wc - x;
+    const double Lf = early ? Le : Lc, Wf = early ? We : Wc;
+    const double Lo = jet ? Lj : P.L0, Wo = jet ? Wj : P.W0;
+    *L = fill ? Lf : Lo;
+    *W = fill ? Wf : Wo;
     *f32 = fill && !early && c32;
 }
 
@@ -678,7 +685,11 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     /* ---------------- clocks, phase, properties ---------------- */
     h.ct += DT;
     h.time += DT;
-    h.phase = h.ct <= h.mx ? REFILL : (h.ct <= h.b1 ? JET : (h.ct <= h.b2 ? COAST : REST));
+    {   /* update_state's if-chain as flat selects, lowest priority first */
+        int ph = h.ct <= h.b2 ? COAST : REST;
+        ph = h.ct <= h.b1 ? JET : ph;
+        h.phase = h.ct <= h.mx ? REFILL : ph;
+    }
     h.pV = h.V;
     h.pv32 = h.g32;
     bool f;
