@@ -527,12 +527,17 @@ SD void cycle_bounds(Hot& h) {
 /* Recording (REC): rec points at this env's column of a trace sample,
  * rec[col * rs] (include/salp.h SalpTraceBuffer); the force columns are
  * written here, the state columns by record_state after the tick. */
-template <bool REC = false, bool RAND = false>
+/* LATE32: read the cycle's float32-mode geometry from LDS only inside the
+ * branch that uses it, not at the top of the tick (no register round trip;
+ * faster in k_rollout, slower in the lock-step kernels: A/B in
+ * profiles/r1f_experiments.md). */
+template <bool REC = false, bool RAND = false, bool LATE32 = false>
 SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_t rs = 0) {
     /* this cycle's float32-mode geometry, used at the end if the lane is in
      * that mode (issued first so that the LDS latency hides under the tick) */
     double k32[C32_N];
-    for (int k = 0; k < C32_N; ++k) k32[k] = c32[k];
+    if (!LATE32)
+        for (int k = 0; k < C32_N; ++k) k32[k] = c32[k];
     const Geo& g = h.geo;
     const double m = g.m;
     /* coefficients of this cycle: the reference's means, or (RAND) the
@@ -703,6 +708,8 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     double com = center_of_mass(P, c, wm, false);
     Geo ng = make_geo_shape(P, c, h.L, h.W, wm, false);
     if (f) {
+        if (LATE32)
+            for (int k = 0; k < C32_N; ++k) k32[k] = c32[k];
         V = k32[C32_V]; wm = k32[C32_WM]; com = k32[C32_COM];
         ng.m = k32[C32_M]; ng.I0 = k32[C32_I0]; ng.I1 = k32[C32_I1];
         ng.kc0 = k32[C32_KC0]; ng.kc1 = k32[C32_KC1]; ng.ra0 = k32[C32_RA0]; ng.ra1 = k32[C32_RA1];

@@ -275,7 +275,7 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
         }
         const Params PV = salp::pin_params(P);
         for (int32_t k = 0; k < A.chunk; ++k)
-            if (h.ct < h.b2) salp::tick<false, RAND>(h, PV, c32);
+            if (h.ct < h.b2) salp::tick<false, RAND, true>(h, PV, c32);
     }
     if (A.B.steps_done) A.B.steps_done[i] = steps;
 }

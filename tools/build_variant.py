@@ -35,7 +35,8 @@ def main():
         open(hit[0], "w").write(s)
     out = os.path.join(ROOT, "exp_build", f"libsalp_{name}.so")
     srcs = [os.path.join(d, "grasp_lab_salp_amd", "csrc", f) for f in ("salp_kernels.hip", "salp_gae.hip")]
-    subprocess.run([B.HIPCC, *B.FLAGS, "-o", out, *srcs], check=True)
+    extra = os.environ.get("EXTRA_FLAGS", "").split()   # e.g. "-mllvm -amdgpu-sched-strategy=max-ilp"
+    subprocess.run([B.HIPCC, *B.FLAGS, *extra, "-o", out, *srcs], check=True)
     print(out)
 
 
