@@ -37,7 +37,7 @@ from torch import nn
 
 from . import _lib
 
-__all__ = ["compute_gae", "ActorCritic", "RolloutBuffer", "PPO", "allreduce_gradients"]
+__all__ = ["compute_gae", "ActorCritic", "SplitKLinear", "RolloutBuffer", "PPO", "allreduce_gradients"]
 
 
 def _ptr(t):
@@ -62,6 +62,48 @@ def compute_gae(rewards, values, episode_starts, last_values, dones, gamma=0.99,
     return adv, ret
 
 
+class _SplitKLinearFn(torch.autograd.Function):
+    """y = x @ W.T + b whose weight gradient is a split-K reduction.
+
+    A minibatch of 32 768 rows makes dW = dY.T @ X a 64x64 (or 64x10) output
+    with K = 32 768: the library picks one or four output tiles and no split-K,
+    so 4 workgroups run a 32 768-long reduction (~120-150 us per GEMM, half of
+    the whole update, profiles/r1m_ppo_kernel_stats.csv).  Here K is cut into
+    `splits` slices reduced by one batched GEMM (64 and more workgroups), and
+    the partial products are summed: same math, different summation order."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, splits):
+        ctx.save_for_backward(x, weight)
+        ctx.splits = splits
+        return torch.addmm(bias, x, weight.t())
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        s = ctx.splits
+        gx = gy @ weight if ctx.needs_input_grad[0] else None
+        r = gy.shape[0] // s
+        gw = torch.bmm(gy.reshape(s, r, -1).transpose(1, 2), x.reshape(s, r, -1)).sum(0)
+        return gx, gw, gy.sum(0), None
+
+
+class SplitKLinear(nn.Linear):
+    """``nn.Linear`` (same parameters, init and forward values) whose weight
+    gradient uses a split-K reduction for large row counts (see
+    :class:`_SplitKLinearFn`); small or ragged batches take ``nn.Linear``'s
+    own path."""
+
+    ROWS_PER_SPLIT = 512
+
+    def forward(self, x):
+        rows = x.shape[0] if x.dim() == 2 else 0
+        s = rows // self.ROWS_PER_SPLIT
+        if torch.is_grad_enabled() and s >= 8 and rows % self.ROWS_PER_SPLIT == 0:
+            return _SplitKLinearFn.apply(x, self.weight, self.bias, s)
+        return super().forward(x)
+
+
 def _ortho(layer, gain):
     nn.init.orthogonal_(layer.weight, gain=gain)
     nn.init.zeros_(layer.bias)
@@ -79,14 +121,14 @@ class ActorCritic(nn.Module):
         def mlp():
             layers, d = [], obs_dim
             for h in hidden:
-                layers += [_ortho(nn.Linear(d, h), math.sqrt(2)), nn.Tanh()]
+                layers += [_ortho(SplitKLinear(d, h), math.sqrt(2)), nn.Tanh()]
                 d = h
             return nn.Sequential(*layers), d
 
         self.pi_net, d_pi = mlp()
         self.vf_net, d_vf = mlp()
-        self.action_net = _ortho(nn.Linear(d_pi, act_dim), 0.01)
-        self.value_net = _ortho(nn.Linear(d_vf, 1), 1.0)
+        self.action_net = _ortho(SplitKLinear(d_pi, act_dim), 0.01)
+        self.value_net = _ortho(SplitKLinear(d_vf, 1), 1.0)
         self.log_std = nn.Parameter(torch.zeros(act_dim))
 
     def value(self, obs):
@@ -170,8 +212,11 @@ class PPO:
                 dist.broadcast(p.data, 0)
         multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
         self.use_graphs = (not multi) if use_graphs is None else bool(use_graphs) and not multi
+        # fused Adam on the GPU: one kernel for all parameters instead of ~4
+        # elementwise kernels per parameter tensor (capturable either way)
+        fused = self.device.type == "cuda"
         self.opt = torch.optim.Adam(self.policy.parameters(), lr=learning_rate, eps=1e-5,
-                                    capturable=self.use_graphs)
+                                    capturable=self.use_graphs, fused=fused or None)
         self._graph = None
         self._graph_warm = 0
         self.n_steps, self.batch_size, self.n_epochs = int(n_steps), int(batch_size), int(n_epochs)
