@@ -225,7 +225,7 @@ class PPO:
         self.normalize_advantage = normalize_advantage
         self.verbose = verbose
         self.reset_nonfinite = reset_nonfinite
-        self.nonfinite_resets = 0
+        self._nonfinite = torch.zeros((), dtype=torch.int64, device=self.device)
         self.gen = g
         self.buf = RolloutBuffer(self.n_steps, self.n_envs, self.obs_dim, self.act_dim, self.device)
         self.low = torch.tensor([0.0, 0.0, -1.0], device=self.device)
@@ -247,12 +247,13 @@ class PPO:
             r = sim.step(torch.clamp(a, self.low, self.high), auto_reset=True, want_terminal_obs=True)
             rew = r.reward.float()
             if self.reset_nonfinite:
-                self._reset_nonfinite(r, rew)
+                rew = self._reset_nonfinite(r, rew)
+            # no host sync in the loop: the bootstrap value is computed for every
+            # env and selected where the episode was truncated, not terminated
             trunc_only = r.truncated & ~r.terminated
-            if bool(trunc_only.any()):
-                with torch.no_grad():
-                    tv = pol.value(r.terminal_obs)
-                rew = torch.where(trunc_only, rew + self.gamma * tv, rew)
+            with torch.no_grad():
+                tv = pol.value(r.terminal_obs)
+            rew = torch.where(trunc_only, rew + self.gamma * tv, rew)
             b.obs[t].copy_(obs)
             b.actions[t].copy_(a)
             b.rewards[t].copy_(rew)
@@ -273,16 +274,21 @@ class PPO:
         tests/test_gpu_parity.py::test_reference_blowup_is_reproduced) and its
         env then returns NaN observations until the 500-cycle timeout.  A
         learner cannot consume those: such envs are reset on the spot and the
-        step is recorded as a truncation with reward 0 and no bootstrap."""
+        step is recorded as a truncation with reward 0 and no bootstrap.
+        Sync-free: the masked reset is a no-op where the mask is all zero."""
         bad = ~torch.isfinite(r.obs).all(1) | ~torch.isfinite(rew)
-        if not bool(bad.any()):
-            return
-        self.nonfinite_resets += int(bad.sum())
+        self._nonfinite = self._nonfinite + bad.sum()
         fresh = self.sim.reset(mask=bad)
-        r.obs[bad] = fresh[bad]
-        rew[bad] = 0.0
-        r.truncated[bad] = True
-        r.terminated[bad] = True     # terminal: no gamma * V(terminal_obs) bootstrap
+        col = bad.unsqueeze(1)
+        r.obs.copy_(torch.where(col, fresh, r.obs))
+        r.truncated |= bad
+        r.terminated |= bad     # terminal: no gamma * V(terminal_obs) bootstrap
+        return torch.where(bad, torch.zeros_like(rew), rew)
+
+    @property
+    def nonfinite_resets(self):
+        """Envs reset because their state diverged (host int; syncs)."""
+        return int(self._nonfinite)
 
     # ----------------------------------------------------------- update
     def _minibatch(self, idx, acc):
