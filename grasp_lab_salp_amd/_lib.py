@@ -75,6 +75,8 @@ SIGNATURES = {
     "salp_math_selftest": (ctypes.c_int, [_V, _V, ctypes.c_int64, _V, _V]),
     "salp_gae": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64, _V, _V, _V, _V, _V, ctypes.c_double,
                                 ctypes.c_double, _V, _V, _V]),
+    "salp_ppo_loss": (ctypes.c_int, [ctypes.c_int64, _V, _V, _V, _V, _V, _V, _V, ctypes.c_double, ctypes.c_double,
+                                     ctypes.c_double, ctypes.c_int, _V, _V, _V, _V, _V]),
 }
 
 

@@ -469,6 +469,12 @@ Params derive(const SalpParams& p, int64_t n, uint64_t seed, int64_t offset) {
 
 }  // namespace
 
+extern "C" __attribute__((visibility("hidden"))) int salp_ppo_loss_launch(
+    int64_t B, const float* mu, const float* log_std, const float* value, const float* actions,
+    const float* old_logp, const float* adv, const float* returns, double clip_range, double ent_coef,
+    double vf_coef, int normalize_advantage, double* workspace, float* out, float* dmu, float* dvalue,
+    void* stream);
+
 extern "C" __attribute__((visibility("hidden"))) int salp_gae_launch(
     int64_t n_steps, int64_t n_envs, const float* rewards, const float* values, const float* episode_starts,
     const float* last_values, const float* last_dones, double gamma, double gae_lambda, float* advantages,
@@ -698,6 +704,21 @@ int salp_bench_ticks(SalpEnv* h, int32_t n_ticks, void* stream) {
 }
 
 int64_t salp_state_ptr(SalpEnv* h) { return h ? (int64_t)(intptr_t)h->state : 0; }
+
+int salp_ppo_loss(int64_t batch, const float* mu, const float* log_std, const float* value,
+                  const float* actions, const float* old_logp, const float* advantages, const float* returns,
+                  double clip_range, double ent_coef, double vf_coef, int normalize_advantage,
+                  double* workspace, float* out, float* dmu, float* dvalue, void* stream) {
+    if (batch <= 0) return fail(nullptr, SALP_EINVAL, "salp_ppo_loss: batch must be positive");
+    if (!mu || !log_std || !value || !actions || !old_logp || !advantages || !returns || !workspace || !out ||
+        !dmu || !dvalue)
+        return fail(nullptr, SALP_EINVAL, "salp_ppo_loss: null buffer");
+    if (!(clip_range >= 0)) return fail(nullptr, SALP_EINVAL, "salp_ppo_loss: clip_range must be >= 0");
+    if (salp_ppo_loss_launch(batch, mu, log_std, value, actions, old_logp, advantages, returns, clip_range, ent_coef,
+                             vf_coef, normalize_advantage, workspace, out, dmu, dvalue, stream) != 0)
+        return fail(nullptr, SALP_EHIP, std::string("k_ppo: ") + hipGetErrorString(hipGetLastError()));
+    return SALP_OK;
+}
 
 int salp_gae(int64_t n_steps, int64_t n_envs, const float* rewards, const float* values,
              const float* episode_starts, const float* last_values, const float* last_dones, double gamma,

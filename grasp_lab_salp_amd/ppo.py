@@ -37,7 +37,7 @@ from torch import nn
 
 from . import _lib
 
-__all__ = ["compute_gae", "ActorCritic", "SplitKLinear", "RolloutBuffer", "PPO", "allreduce_gradients"]
+__all__ = ["compute_gae", "ppo_loss", "torch_ppo_loss", "ActorCritic", "SplitKLinear", "RolloutBuffer", "PPO", "allreduce_gradients"]
 
 
 def _ptr(t):
@@ -102,6 +102,72 @@ class SplitKLinear(nn.Linear):
         if torch.is_grad_enabled() and s >= 8 and rows % self.ROWS_PER_SPLIT == 0:
             return _SplitKLinearFn.apply(x, self.weight, self.bias, s)
         return super().forward(x)
+
+
+class _FusedPPOLossFn(torch.autograd.Function):
+    """SB3 PPO loss head through the HIP kernels of ``salp_ppo_loss``: the
+    forward pass also produces d loss / d (mu, log_std, value), which the
+    backward pass only scales.  Outputs (loss, stats[pg, vf, entropy,
+    clip_fraction]); stats carry no gradient."""
+
+    @staticmethod
+    def forward(ctx, mu, log_std, value, actions, old_logp, adv, returns, clip, ent_coef, vf_coef, normalize):
+        B = mu.shape[0]
+        dev = mu.device
+        out = torch.empty(8, dtype=torch.float32, device=dev)
+        dmu = torch.empty_like(mu)
+        dv = torch.empty_like(value)
+        ws = torch.empty(_PPO_WS, dtype=torch.float64, device=dev)
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        _lib.check(_lib.load().salp_ppo_loss(B, _ptr(mu), _ptr(log_std), _ptr(value), _ptr(actions),
+                                             _ptr(old_logp), _ptr(adv), _ptr(returns), float(clip),
+                                             float(ent_coef), float(vf_coef), int(bool(normalize)), _ptr(ws),
+                                             _ptr(out), _ptr(dmu), _ptr(dv), stream))
+        ctx.save_for_backward(dmu, dv, out)
+        stats = out[1:5].clone()
+        ctx.mark_non_differentiable(stats)
+        return out[0].clone(), stats
+
+    @staticmethod
+    def backward(ctx, g_loss, g_stats):
+        dmu, dv, out = ctx.saved_tensors
+        return dmu * g_loss, out[5:8] * g_loss, dv * g_loss, None, None, None, None, None, None, None, None
+
+
+_PPO_WS = 2048   # include/salp.h SALP_PPO_WORKSPACE_DOUBLES
+
+
+def ppo_loss(mu, log_std, value, actions, old_logp, advantages, returns, clip_range, ent_coef, vf_coef,
+             normalize_advantage):
+    """Fused SB3 PPO loss (``salp_ppo_loss``): returns (loss, stats) with
+    stats = [pg_loss, vf_loss, entropy, clip_fraction]; differentiable in mu
+    [B,3], log_std [3] and value [B].  CUDA float32 tensors."""
+    ts = (mu, log_std, value, actions, old_logp, advantages, returns)
+    B = mu.shape[0]
+    shapes = ((B, 3), (3,), (B,), (B, 3), (B,), (B,), (B,))
+    for t, shp in zip(ts, shapes):
+        if not t.is_cuda or t.dtype != torch.float32 or tuple(t.shape) != shp:
+            raise ValueError(f"ppo_loss: expected a float32 CUDA tensor of shape {shp}, got {tuple(t.shape)}")
+    return _FusedPPOLossFn.apply(*(t.contiguous() for t in ts), clip_range, ent_coef, vf_coef,
+                                 normalize_advantage)
+
+
+def torch_ppo_loss(mu, log_std, value, actions, old_logp, advantages, returns, clip_range, ent_coef, vf_coef,
+                   normalize_advantage):
+    """The same loss as torch ops (SB3 PPO.train), the reference for ppo_loss."""
+    d = torch.distributions.Normal(mu, log_std.exp().expand_as(mu), validate_args=False)
+    lp = d.log_prob(actions).sum(-1)
+    ent = d.entropy().sum(-1)
+    adv = advantages
+    if normalize_advantage and adv.numel() > 1:
+        adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+    ratio = torch.exp(lp - old_logp)
+    pg = -torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - clip_range, 1 + clip_range)).mean()
+    vf = torch.nn.functional.mse_loss(returns, value)
+    ent_loss = -ent.mean()
+    loss = pg + ent_coef * ent_loss + vf_coef * vf
+    clip = ((ratio - 1).abs() > clip_range).float().mean()
+    return loss, torch.stack([pg.detach(), vf.detach(), -ent_loss.detach(), clip.detach()])
 
 
 def _ortho(layer, gain):
@@ -194,7 +260,7 @@ class PPO:
     def __init__(self, policy, env, learning_rate=3e-4, n_steps=2048, batch_size=64, n_epochs=10, gamma=0.99,
                  gae_lambda=0.95, clip_range=0.2, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5,
                  normalize_advantage=True, seed=0, device=None, verbose=0, reset_nonfinite=True,
-                 use_graphs=None):
+                 use_graphs=None, fused_loss=None):
         if policy not in ("MlpPolicy", None) and not isinstance(policy, nn.Module):
             raise ValueError("policy must be 'MlpPolicy' or an nn.Module")
         self.env = env
@@ -223,6 +289,10 @@ class PPO:
         self.gamma, self.gae_lambda, self.clip_range = gamma, gae_lambda, clip_range
         self.ent_coef, self.vf_coef, self.max_grad_norm = ent_coef, vf_coef, max_grad_norm
         self.normalize_advantage = normalize_advantage
+        # the loss head runs as the fused HIP kernels of salp_ppo_loss for the
+        # built-in policy on a GPU; torch ops otherwise (custom policies)
+        self.fused_loss = (self.device.type == "cuda" and isinstance(self.policy, ActorCritic)
+                           if fused_loss is None else bool(fused_loss))
         self.verbose = verbose
         self.reset_nonfinite = reset_nonfinite
         self._nonfinite = torch.zeros((), dtype=torch.int64, device=self.device)
@@ -296,21 +366,30 @@ class PPO:
         (pg_loss, vf_loss, entropy, clip_fraction) to `acc`."""
         b, pol = self.buf, self.policy
         N = self.n_steps * self.n_envs
-        v, lp, ent = pol.evaluate(b.obs.reshape(N, -1)[idx], b.actions.reshape(N, -1)[idx])
-        adv = b.advantages.reshape(N)[idx]
-        if self.normalize_advantage and idx.numel() > 1:
-            adv = (adv - adv.mean()) / (adv.std() + 1e-8)
-        ratio = torch.exp(lp - b.log_probs.reshape(N)[idx])
-        pg = -torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - self.clip_range, 1 + self.clip_range)).mean()
-        vf = torch.nn.functional.mse_loss(b.returns.reshape(N)[idx], v)
-        ent_loss = -ent.mean()
-        loss = pg + self.ent_coef * ent_loss + self.vf_coef * vf
+        obs, act = b.obs.reshape(N, -1)[idx], b.actions.reshape(N, -1)[idx]
+        rows = (b.log_probs.reshape(N)[idx], b.advantages.reshape(N)[idx], b.returns.reshape(N)[idx])
+        norm = self.normalize_advantage and idx.numel() > 1
+        if self.fused_loss:
+            mean = pol.action_net(pol.pi_net(obs))
+            loss, stats = ppo_loss(mean, pol.log_std, pol.value(obs), act, *rows, self.clip_range, self.ent_coef,
+                                   self.vf_coef, norm)
+        else:   # any policy exposing evaluate(obs, actions) -> (value, log_prob, entropy)
+            v, lp, ent = pol.evaluate(obs, act)
+            old_lp, adv, ret = rows
+            if norm:
+                adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+            ratio = torch.exp(lp - old_lp)
+            pg = -torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - self.clip_range, 1 + self.clip_range)).mean()
+            vf = torch.nn.functional.mse_loss(ret, v)
+            ent_loss = -ent.mean()
+            loss = pg + self.ent_coef * ent_loss + self.vf_coef * vf
+            clip = ((ratio - 1).abs() > self.clip_range).float().mean()
+            stats = torch.stack([pg.detach(), vf.detach(), -ent_loss.detach(), clip.detach()])
         loss.backward()
         allreduce_gradients(list(pol.parameters()))
         nn.utils.clip_grad_norm_(pol.parameters(), self.max_grad_norm)
         self.opt.step()
-        clip = ((ratio - 1).abs() > self.clip_range).float().mean()
-        acc += torch.stack([pg.detach(), vf.detach(), -ent_loss.detach(), clip.detach()])
+        acc += stats
 
     def _graphed_minibatch(self, idx):
         """The same step through a HIP graph: three eager warm-up steps on a

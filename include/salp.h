@@ -159,6 +159,23 @@ int salp_gae(int64_t n_steps, int64_t n_envs, const float* rewards, const float*
              const float* episode_starts, const float* last_values, const float* last_dones,
              double gamma, double gae_lambda, float* advantages, float* returns, void* stream);
 
+/* Fused PPO loss head (stable_baselines3 PPO.train's clipped surrogate, value
+ * MSE and entropy for a diagonal Gaussian with state-independent log-std) and
+ * its gradient, for one minibatch of B rows.  Device float32 arrays: mu [B][3]
+ * (policy mean), log_std [3], value [B], actions [B][3], old_logp [B],
+ * advantages [B], returns [B].  normalize_advantage: SB3's per-minibatch
+ * (adv - mean) / (std + 1e-8).  workspace: SALP_PPO_WORKSPACE_DOUBLES doubles.
+ * Outputs: out [8] = loss, pg_loss, vf_loss, entropy, clip_fraction,
+ * d loss / d log_std [3]; dmu [B][3] = d loss / d mu; dvalue [B] = d loss /
+ * d value.  Float32 row math with fp64 sums (agrees with the torch expression
+ * to float32 rounding).  Not part of the reference's API: it is the loss of
+ * the SB3 learner the reference trains with (grasp_lab_salp_amd/ppo.py). */
+#define SALP_PPO_WORKSPACE_DOUBLES 2048
+int salp_ppo_loss(int64_t batch, const float* mu, const float* log_std, const float* value,
+                  const float* actions, const float* old_logp, const float* advantages, const float* returns,
+                  double clip_range, double ent_coef, double vf_coef, int normalize_advantage,
+                  double* workspace, float* out, float* dmu, float* dvalue, void* stream);
+
 /* ------------------------------------------------ Robot / Nozzle level */
 /* The reference's Robot API for callers that drive the robot directly,
  * without the task env (src/compare_trajectories.py:120-168,

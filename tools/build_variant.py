@@ -24,7 +24,7 @@ def main():
         shutil.rmtree(d)
     shutil.copytree(os.path.join(ROOT, "grasp_lab_salp_amd", "csrc"), os.path.join(d, "grasp_lab_salp_amd", "csrc"))
     shutil.copytree(os.path.join(ROOT, "include"), os.path.join(d, "include"))
-    files = [os.path.join(d, "grasp_lab_salp_amd", "csrc", f) for f in ("salp_kernels.hip", "salp_device.h", "salp_gae.hip", "salp_math.h")]
+    files = [os.path.join(d, "grasp_lab_salp_amd", "csrc", f) for f in ("salp_kernels.hip", "salp_device.h", "salp_gae.hip", "salp_math.h", "salp_ppo.hip")]
     for r in reps:
         old, new = r.split("=>", 1)
         old, new = old.replace("\\n", "\n"), new.replace("\\n", "\n")
@@ -34,7 +34,7 @@ def main():
         s = open(hit[0]).read().replace(old, new)
         open(hit[0], "w").write(s)
     out = os.path.join(ROOT, "exp_build", f"libsalp_{name}.so")
-    srcs = [os.path.join(d, "grasp_lab_salp_amd", "csrc", f) for f in ("salp_kernels.hip", "salp_gae.hip")]
+    srcs = [os.path.join(d, "grasp_lab_salp_amd", "csrc", f) for f in ("salp_kernels.hip", "salp_gae.hip", "salp_ppo.hip")]
     extra = os.environ.get("EXTRA_FLAGS", "").split()   # e.g. "-mllvm -amdgpu-sched-strategy=max-ilp"
     subprocess.run([B.HIPCC, *B.FLAGS, *extra, "-o", out, *srcs], check=True)
     print(out)
