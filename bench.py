@@ -1,8 +1,16 @@
 """Throughput of the SALP env-step hot path on MI355X (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
-    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
+
+`--gpus N` (N > 1) without torchrun's environment starts N ranks itself: it
+runs `torch.distributed.run` as a child process before anything touches the
+GPU and exits with its status.  Each rank drives one GPU (RCCL process group,
+`nccl` backend) and owns the global env ids [rank * n, (rank + 1) * n).  This
+replaces the reference's 8 SubprocVecEnv workers (src/train_robot.py:25-26).
+`--dry-run` runs the same launcher and reductions on the CPU (gloo, no GPU
+kernels): the multi-rank plumbing test of tests/test_bench_launcher.py.
 
 Workload (BASELINE.json configs[2]): 65 536 envs per GPU, canonical robot and
 env of src/train_robot.py:11-21, synthetic random actions U(action box) from
@@ -17,18 +25,21 @@ the final counter reductions.
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import torch  # noqa: E402
+import torch  # noqa: E402  (importing torch does not initialise the GPU)
 import torch.distributed as dist  # noqa: E402
 
 from grasp_lab_salp_amd._abi import FIELD, default_params  # noqa: E402
-from grasp_lab_salp_amd.shard import env_id_offset, reduce_run  # noqa: E402
+from grasp_lab_salp_amd.shard import env_id_offset, reduce_run, reduce_sums  # noqa: E402
 
+METRIC = "env-steps/sec at 65536 parallel envs, 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X fp64 vector spec (half the 157.3 TF fp32 rate)
 # compulsory bytes per env-step B = 2 * S + outputs, S = the
@@ -37,6 +48,16 @@ FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X fp64 vector spec (half the 157.3 TF fp32 
 STATE_BYTES = FIELD["cd"] * 8
 STEP_OUT_BYTES = 10 * 4 + 3 * 4 + 4 + 1   # obs + action + reward(f32) + done per env-step
 BYTES_PER_ENV_STEP = 2 * STATE_BYTES + STEP_OUT_BYTES
+# Algorithmic fp64 work of one physics tick ("F_TICK"): the
+# reference's operations (src/robot.py:789-875, src/dynamics.py, src/geometry.py)
+# with structural zeros removed; +,-,*,/,sqrt,sin,cos each one flop-equivalent.
+# Newton 101 + Euler 98 + integration 90 + clock/phase 5 + geometry 93 (a tick
+# outside JET; a JET tick adds 11).
+F_TICK_ALGO = 387
+# Mean ticks per env-step under the synthetic action distribution: the oracle
+# over 3 seeds x 4096 envs x 20 env-steps (245 760 env-steps) gives 710.4.
+MEAN_TICKS_PER_ENV_STEP = 710.4
+HOT_FIELDS = slice(FIELD["v0"], FIELD["ang2"] + 1)   # kinematic state: NaN once an env diverged
 
 
 def pmc_profile(n, budget, chunk):
@@ -54,9 +75,9 @@ def pmc_profile(n, budget, chunk):
     return best
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one GPU each); >1 self-launches torchrun")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n-envs", type=int, default=65536, help="envs per GPU")
@@ -67,36 +88,150 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-lockstep", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher + reductions only, gloo on the CPU, no GPU kernels")
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(a, argv):
+    """Start `a.gpus` ranks of this script under torch.distributed.run (a child
+    process; this process never touches the GPU) and return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except AttributeError:
+        allowed = os.cpu_count()
+    return {"model": model, "logical_cpus": os.cpu_count(), "cpus_allowed": allowed}
+
+
+def cpu_threads():
+    """Host cores this job may use: the scheduler's share (OMP_NUM_THREADS, set
+    to the box's per-GPU CPU share on the GPU pool) or, without it, every CPU
+    in this process's affinity mask."""
+    env = os.environ.get("SALP_CPU_THREADS") or os.environ.get("OMP_NUM_THREADS")
+    if env:
+        return max(1, int(env))
+    return cpu_info()["cpus_allowed"] or 1
 
 
 def cpu_baseline(seconds):
-    """The C oracle (reference restatement) on the host cores, bounded sample."""
+    """The C oracle (the reference's algorithm restated, oracle/salp_oracle.c)
+    on the host cores, bounded samples, seeds 0/1/2:
+      * config 1 (BASELINE.json configs[0]): 1 env x 1000 random-action
+        env-steps on one core, the robot of src/test_robot.py:6-9 (== make_env);
+      * throughput: 64 envs per thread, OpenMP over every core this job has,
+        `seconds` split over the three seeds."""
     from oracle.oracle import Oracle
-    threads = int(os.environ.get("SALP_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    threads = cpu_threads()
+    p = default_params()
+    # untimed warm-up: the first OpenMP region pays the thread-pool start (~1 s)
+    w = Oracle(p, 64 * threads, seed=99)
+    w.reset()
+    w.step_random(1, threads=threads)
     n = 64 * threads
-    o = Oracle(default_params(), n, seed=123)
-    o.reset()
-    steps, ticks, t0 = 0, 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        _, tk = o.step_random(1, threads=threads)
-        steps += n
-        ticks += tk
-    dt = time.perf_counter() - t0
-    return {"value": steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{n} envs x {steps // n} random-action env-steps ({ticks} ticks, "
-                      f"{dt:.1f} s) of the oracle C restatement, OpenMP {threads} threads",
-            "ticks_per_sec": ticks / dt}
+    per_seed = []
+    for seed in (0, 1, 2):
+        o = Oracle(p, n, seed=seed)
+        o.reset()
+        w.step_random(1, threads=threads)   # untimed, keeps the thread pool hot
+        steps, ticks, t0 = 0, 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds / 3:
+            _, tk = o.step_random(1, threads=threads)
+            steps += n
+            ticks += tk
+        dt = time.perf_counter() - t0
+        per_seed.append({"seed": seed, "env_steps": steps, "ticks": ticks, "seconds": dt,
+                         "env_steps_per_sec": steps / dt})
+    cfg1 = []
+    for seed in (0, 1, 2):
+        o = Oracle(p, 1, seed=seed)
+        o.reset()
+        t0 = time.perf_counter()
+        _, tk = o.step_random(1000, threads=1)
+        dt = time.perf_counter() - t0
+        cfg1.append({"seed": seed, "seconds": dt, "env_steps_per_sec": 1000 / dt, "ticks": tk})
+    steps = sum(s["env_steps"] for s in per_seed)
+    secs = sum(s["seconds"] for s in per_seed)
+    ticks = sum(s["ticks"] for s in per_seed)
+    value = steps / secs
+    return {"value": value, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "per_core": value / threads, "ticks_per_sec": ticks / secs, "cpu": cpu_info(),
+            "sample": f"oracle C restatement, OpenMP {threads} threads, {n} envs x random-action env-steps, "
+                      f"seeds 0/1/2 ({secs:.1f} s); config 1 = 1 env x 1000 env-steps on one core",
+            "per_seed": per_seed,
+            "config1": {"env_steps": 1000, "per_seed": cfg1,
+                        "env_steps_per_sec": 3000 / sum(c["seconds"] for c in cfg1)},
+            "note": "cores = the CPU share the GPU pool grants a one-GPU job (OMP_NUM_THREADS); "
+                    "the interpreted Python reference itself does ~2.1 env-steps/s per core (SURVEY.md §6)"}
 
 
-def main():
-    a = parse()
+def dry_run(a, world, rank):
+    """Launcher plumbing without a GPU: same rank layout, offsets and
+    reductions as the real run, over gloo."""
+    n = a.n_envs
+    off = env_id_offset(rank, n)
+    offs = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(offs, torch.tensor([off], dtype=torch.int64))
+    else:
+        offs = [torch.tensor([off])]
+    elapsed, steps_total, _, _ = reduce_run(1.0 + rank, float(n), 0.0, None)
+    seen = dist.get_world_size() if world > 1 else 1
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "dry_run": True, "value": None, "unit": "env-steps/s",
+                          "n_gpus": world, "world_size": seen, "steps": a.steps, "warmup": a.warmup,
+                          "env_id_offsets": [int(o) for o in offs], "max_elapsed": elapsed,
+                          "env_steps_sum": steps_total, "backend": "gloo" if world > 1 else None}), flush=True)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    if a.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started {world} ranks")
+    if a.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo")
+        dry_run(a, world, rank)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if dist.get_world_size() != world:
+            raise SystemExit("process group size differs from WORLD_SIZE")
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -122,13 +257,15 @@ def main():
     barrier()
     torch.cuda.synchronize()
     s0 = int(done.sum())
+    # HIP events on the stream the kernel is launched on (torch's current stream)
+    stream = torch.cuda.current_stream(dev)
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
     t0 = time.perf_counter()
     for k in range(a.steps):
-        starts[k].record()
+        starts[k].record(stream)
         env.rollout(a.tick_budget, buffers=bufs, steps_done=done, chunk=a.chunk)
-        ends[k].record()
+        ends[k].record(stream)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     barrier()
@@ -136,33 +273,45 @@ def main():
     steps_local = int(done.sum()) - s0
     kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / a.steps
 
+    # SURVEY.md §5 failure detection: envs whose explicit integration diverged
+    # (the reference's own blow-up, test_reference_blowup_is_reproduced) at
+    # the end of the run, and the non-finite observations among the last
+    # `cap` env-steps of every env held in the rollout buffer.
+    st = env.get_state()
+    diverged = int((~torch.isfinite(st[HOT_FIELDS]).all(0)).sum())
+    bad_rows = int((~torch.isfinite(bufs["obs"]).all(-1)).sum())
+
     # lock-step drop-in path (one env-step per env per launch) for reference
     lock = None
     if not a.no_lockstep:
         env.step_random(1)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
+        e0.record(stream)
         env.step_random(4)
-        e1.record()
+        e1.record(stream)
         torch.cuda.synchronize()
         lock = 4 * n / (e0.elapsed_time(e1) / 1e3)
 
     elapsed, steps_total, kern_ms, lock_total = reduce_run(elapsed, steps_local, kern_ms, lock, device=dev)
+    diverged_total, bad_rows_total = reduce_sums([diverged, bad_rows], device=dev)
+    seen_world = dist.get_world_size() if world > 1 else 1
     if rank != 0:
         dist.destroy_process_group()
         return
 
     prof = pmc_profile(n, a.tick_budget, a.chunk)
-    ticks_total = float(-(-a.tick_budget // a.chunk) * a.chunk) * n * a.steps * world
+    budget_ticks = float(-(-a.tick_budget // a.chunk) * a.chunk) * n * a.steps * world
     steps_per_launch = steps_local / a.steps
     bytes_launch = steps_per_launch * BYTES_PER_ENV_STEP
     achieved = bytes_launch / (kern_ms / 1e3) / 1e9
+    env_ticks_per_launch = steps_per_launch * MEAN_TICKS_PER_ENV_STEP
     res = {
-        "metric": "env-steps/sec at 65536 parallel envs, 1/2/4/8 MI355X; % HBM roofline",
+        "metric": METRIC,
         "value": steps_total / elapsed,
         "unit": "env-steps/s",
         "n_gpus": world,
+        "world_size": seen_world,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": elapsed / a.steps * 1e3,
@@ -175,8 +324,8 @@ def main():
                                "canonical make_env robot (src/train_robot.py:11-21), 2 obstacles",
                    "n_envs_per_gpu": n, "tick_budget": a.tick_budget, "chunk": a.chunk, "rollout_capacity": cap,
                    "parallelism": f"env-shard x{world}"},
-        "ticks_per_sec": ticks_total / elapsed,
-        "mean_ticks_per_env_step": ticks_total / max(steps_total, 1.0),
+        "ticks_per_sec": steps_total * MEAN_TICKS_PER_ENV_STEP / elapsed,
+        "budget_ticks_per_sec": budget_ticks / elapsed,
         "kernel_ms_per_launch": kern_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
@@ -187,14 +336,32 @@ def main():
                      "note": "algorithmic bytes = env-steps per launch x (2 x 816 B state + 57 B outputs) "
                              "(SURVEY 8(d)); the kernel is fp64-VALU bound (see roofline_valu)"},
         "lockstep_env_steps_per_sec": lock_total,
+        "divergence": {"diverged_envs_at_end": diverged_total, "envs": n * world,
+                       "nonfinite_obs_rows_in_buffer": bad_rows_total, "buffer_rows": cap * n * world,
+                       "note": "the reference integrator itself diverges for some actions (jet_time < dt); "
+                               "such envs carry NaN until the 500-cycle timeout resets them"},
     }
-    f_tick = prof[1]["derived"].get("fp64_flops_per_env_tick") if prof else None
-    if f_tick:
-        # executed fp64 flops (PMC, FMA = 2) per env-tick of budget x this run's kernel time
-        fl = f_tick * float(a.tick_budget) * n / (kern_ms / 1e3) / 1e12
-        res["roofline_valu"] = {"bound": "fp64-valu", "achieved": fl, "peak": FP64_VALU_PEAK_TFLOPS,
-                                "unit": "TFLOP/s", "frac": fl / FP64_VALU_PEAK_TFLOPS,
-                                "flops_per_env_tick": f_tick, "source": prof[0]}
+    # fp64 VALU roofline: algorithmic flops (F_TICK_ALGO per executed env-tick)
+    # and, where a PMC summary of this configuration exists, executed flops
+    fl_algo = F_TICK_ALGO * env_ticks_per_launch / (kern_ms / 1e3) / 1e12
+    res["roofline_valu"] = {"bound": "fp64-valu", "achieved": fl_algo, "peak": FP64_VALU_PEAK_TFLOPS,
+                            "unit": "TFLOP/s", "frac": fl_algo / FP64_VALU_PEAK_TFLOPS,
+                            "flops_per_env_tick": F_TICK_ALGO, "count": "algorithmic (DESIGN.md §5)"}
+    if prof:
+        d = prof[1]["derived"]
+        per = prof[1]["per_dispatch"]
+        if d.get("fp64_flops"):
+            fl = d["fp64_flops"] / (kern_ms / 1e3) / 1e12
+            mix = {k.replace("SQ_INSTS_VALU_", "").lower(): per[k]["mean"] / max(d["fp64_valu_insts"], 1.0)
+                   for k in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
+                             "SQ_INSTS_VALU_TRANS_F64") if k in per}
+            res["roofline_valu"]["executed"] = {
+                "achieved": fl, "frac": fl / FP64_VALU_PEAK_TFLOPS,
+                "flops_per_env_tick": d.get("fp64_flops_per_env_tick"), "instruction_mix": mix,
+                "active_valu_frac": d.get("active_valu_frac"), "waves": per.get("SQ_WAVES", {}).get("mean"),
+                "source": prof[0],
+                "note": "PMC fp64 VALU instructions x 64 lanes (FMA = 2): both arms of branch-free selects, "
+                        "Newton steps of divisions and polynomial transcendentals included"}
     if world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(a.cpu_baseline_seconds)
     print(json.dumps(res), flush=True)

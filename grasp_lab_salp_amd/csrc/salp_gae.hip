@@ -88,7 +88,8 @@ __global__ __launch_bounds__(kGaeBlock) void k_gae(int64_t T, int64_t n, const f
 
 }  // namespace
 
-extern "C" __attribute__((visibility("hidden"))) int salp_gae_launch(int64_t n_steps, int64_t n_envs, const float* rewards, const float* values,
+// Returns the launch status; the caller reports it (salp_kernels.hip).
+extern "C" __attribute__((visibility("hidden"))) hipError_t salp_gae_launch(int64_t n_steps, int64_t n_envs, const float* rewards, const float* values,
                                const float* episode_starts, const float* last_values,
                                const float* last_dones, double gamma, double gae_lambda, float* advantages,
                                float* returns, void* stream) {
@@ -105,5 +106,5 @@ extern "C" __attribute__((visibility("hidden"))) int salp_gae_launch(int64_t n_s
     const unsigned blocks = (unsigned)((n_envs + bs - 1) / bs);
     hipLaunchKernelGGL(k_gae, dim3(blocks), dim3((unsigned)bs), 0, (hipStream_t)stream, n_steps, n_envs, rewards,
                        values, episode_starts, last_values, last_dones, g, gl, advantages, returns);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
+    return hipGetLastError();
 }

@@ -469,13 +469,13 @@ Params derive(const SalpParams& p, int64_t n, uint64_t seed, int64_t offset) {
 
 }  // namespace
 
-extern "C" __attribute__((visibility("hidden"))) int salp_ppo_loss_launch(
+extern "C" __attribute__((visibility("hidden"))) hipError_t salp_ppo_loss_launch(
     int64_t B, const float* mu, const float* log_std, const float* value, const float* actions,
     const float* old_logp, const float* adv, const float* returns, double clip_range, double ent_coef,
     double vf_coef, int normalize_advantage, double* workspace, float* out, float* dmu, float* dvalue,
     void* stream);
 
-extern "C" __attribute__((visibility("hidden"))) int salp_gae_launch(
+extern "C" __attribute__((visibility("hidden"))) hipError_t salp_gae_launch(
     int64_t n_steps, int64_t n_envs, const float* rewards, const float* values, const float* episode_starts,
     const float* last_values, const float* last_dones, double gamma, double gae_lambda, float* advantages,
     float* returns, void* stream);
@@ -714,10 +714,10 @@ int salp_ppo_loss(int64_t batch, const float* mu, const float* log_std, const fl
         !dmu || !dvalue)
         return fail(nullptr, SALP_EINVAL, "salp_ppo_loss: null buffer");
     if (!(clip_range >= 0)) return fail(nullptr, SALP_EINVAL, "salp_ppo_loss: clip_range must be >= 0");
-    if (salp_ppo_loss_launch(batch, mu, log_std, value, actions, old_logp, advantages, returns, clip_range, ent_coef,
-                             vf_coef, normalize_advantage, workspace, out, dmu, dvalue, stream) != 0)
-        return fail(nullptr, SALP_EHIP, std::string("k_ppo: ") + hipGetErrorString(hipGetLastError()));
-    return SALP_OK;
+    const hipError_t e = salp_ppo_loss_launch(batch, mu, log_std, value, actions, old_logp, advantages, returns,
+                                              clip_range, ent_coef, vf_coef, normalize_advantage, workspace, out, dmu,
+                                              dvalue, stream);
+    return check_hip(nullptr, e, "k_ppo");
 }
 
 int salp_gae(int64_t n_steps, int64_t n_envs, const float* rewards, const float* values,
@@ -727,10 +727,9 @@ int salp_gae(int64_t n_steps, int64_t n_envs, const float* rewards, const float*
     if (!rewards || !values || !episode_starts || !last_values || !last_dones || !advantages || !returns)
         return fail(nullptr, SALP_EINVAL, "salp_gae: null buffer");
     if (n_steps == 0 || n_envs == 0) return SALP_OK;
-    if (salp_gae_launch(n_steps, n_envs, rewards, values, episode_starts, last_values, last_dones, gamma,
-                        gae_lambda, advantages, returns, stream) != 0)
-        return fail(nullptr, SALP_EHIP, std::string("k_gae: ") + hipGetErrorString(hipGetLastError()));
-    return SALP_OK;
+    const hipError_t e = salp_gae_launch(n_steps, n_envs, rewards, values, episode_starts, last_values, last_dones,
+                                         gamma, gae_lambda, advantages, returns, stream);
+    return check_hip(nullptr, e, "k_gae");
 }
 
 }  // extern "C"

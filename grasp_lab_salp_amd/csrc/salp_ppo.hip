@@ -155,7 +155,10 @@ static_assert(kPpoGrid <= kPpoBlock, "k_ppo_final reduces one partial per thread
 
 }  // namespace
 
-extern "C" __attribute__((visibility("hidden"))) int salp_ppo_loss_launch(
+// Returns the launch status (hipSuccess or the error the launches left); the
+// caller builds its message from this value, not from a second
+// hipGetLastError() (which would read the already-cleared error).
+extern "C" __attribute__((visibility("hidden"))) hipError_t salp_ppo_loss_launch(
     int64_t B, const float* mu, const float* log_std, const float* value, const float* actions,
     const float* old_logp, const float* adv, const float* returns, double clip_range, double ent_coef,
     double vf_coef, int normalize_advantage, double* workspace, float* out, float* dmu, float* dvalue,
@@ -169,5 +172,5 @@ extern "C" __attribute__((visibility("hidden"))) int salp_ppo_loss_launch(
                        dvalue);
     hipLaunchKernelGGL(k_ppo_final, dim3(1), dim3(kPpoBlock), 0, s, B, log_std, (float)ent_coef, (float)vf_coef,
                        row_part, out);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
+    return hipGetLastError();
 }

@@ -36,8 +36,10 @@ import torch.distributed as dist
 from torch import nn
 
 from . import _lib
+from ._abi import INFO
 
-__all__ = ["compute_gae", "ppo_loss", "torch_ppo_loss", "ActorCritic", "SplitKLinear", "RolloutBuffer", "PPO", "allreduce_gradients"]
+__all__ = ["compute_gae", "ppo_loss", "torch_ppo_loss", "ActorCritic", "SplitKLinear", "RolloutBuffer", "PPO",
+           "allreduce_gradients", "sampling_generator", "timeout_bootstrap", "diverged_mask"]
 
 
 def _ptr(t):
@@ -135,6 +137,7 @@ class _FusedPPOLossFn(torch.autograd.Function):
 
 
 _PPO_WS = 2048   # include/salp.h SALP_PPO_WORKSPACE_DOUBLES
+_EP_RETURN = INFO["ep_return"]
 
 
 def ppo_loss(mu, log_std, value, actions, old_logp, advantages, returns, clip_range, ent_coef, vf_coef,
@@ -205,14 +208,58 @@ class ActorCritic(nn.Module):
         return torch.distributions.Normal(mean, self.log_std.exp().expand_as(mean), validate_args=False)
 
     @torch.no_grad()
-    def act(self, obs):
+    def act(self, obs, generator=None):
+        """(action, value, log_prob); the Gaussian noise comes from `generator`
+        when given (Normal.sample draws mean + std * N(0, 1) the same way)."""
         d = self.dist(obs)
-        a = d.sample()
+        if generator is None:
+            a = d.sample()
+        else:
+            a = d.mean + d.stddev * torch.randn(d.mean.shape, generator=generator, device=d.mean.device,
+                                                dtype=d.mean.dtype)
         return a, self.value(obs), d.log_prob(a).sum(-1)
 
     def evaluate(self, obs, actions):
         d = self.dist(obs)
         return self.value(obs), d.log_prob(actions).sum(-1), d.entropy().sum(-1)
+
+
+def sampling_generator(seed, device):
+    """The exploration-noise generator of one rank: seeded with (seed, rank),
+    so ranks that share initial weights still draw independent actions for
+    their own envs (a shared seed would correlate the noise of env i on every
+    rank).  Rank 0 of a run keeps the single-process stream."""
+    rank = dist.get_rank() if (dist.is_available() and dist.is_initialized()) else 0
+    g = torch.Generator(device=device)
+    g.manual_seed(int(seed) + 1_000_003 * int(rank))
+    return g
+
+
+def timeout_bootstrap(reward, terminated, truncated, terminal_value, gamma):
+    """SB3 ``collect_rollouts``' handling of time limits: an episode cut by
+    truncation (not termination) gets ``gamma * V(terminal_obs)`` added to its
+    last reward, so GAE does not treat the time limit as a real end.
+    Branch-free over the batch (no host sync)."""
+    trunc_only = truncated & ~terminated
+    return torch.where(trunc_only, reward + gamma * terminal_value, reward)
+
+
+# Learner-side divergence guard.  The reference integrator diverges for some
+# actions (jet_time < dt; tests/test_gpu_parity.py::test_reference_blowup_is_
+# reproduced): velocities grow by orders of magnitude for many ticks before
+# they overflow to inf/NaN, so an env on its way there first returns huge
+# FINITE rewards (100 * (prev_dist - dist), -100 * |avg v_y|) and observations.
+# A legitimate step stays far inside these bounds: |reward| <= ~1.5e3 (success
+# +500, progress and penalties of a body moving < 1 m/s within 5 m of the
+# target), |obs| < 1e2 (metres, m/s, rad).
+DIVERGED_OBS_ABS = 1e3
+DIVERGED_REWARD_ABS = 1e4
+
+
+def diverged_mask(obs, reward):
+    """Envs whose step shows divergence: non-finite, or beyond the bounds above."""
+    return (~torch.isfinite(obs).all(1) | ~torch.isfinite(reward) | (obs.abs() > DIVERGED_OBS_ABS).any(1)
+            | (reward.abs() > DIVERGED_REWARD_ABS))
 
 
 class RolloutBuffer:
@@ -263,6 +310,10 @@ class PPO:
                  use_graphs=None, fused_loss=None):
         if policy not in ("MlpPolicy", None) and not isinstance(policy, nn.Module):
             raise ValueError("policy must be 'MlpPolicy' or an nn.Module")
+        if fused_loss and isinstance(policy, nn.Module) and not all(
+                hasattr(policy, k) for k in ("action_net", "pi_net", "log_std", "value")):
+            raise ValueError("fused_loss=True needs an ActorCritic-shaped policy (action_net, pi_net, log_std, "
+                             "value); pass fused_loss=False for a custom policy")
         self.env = env
         self.sim = getattr(env, "sim", env)
         self.device = self.sim.device if device is None else torch.device(device)
@@ -276,6 +327,8 @@ class PPO:
         if dist.is_available() and dist.is_initialized():   # identical initial weights on every rank
             for p in self.policy.parameters():
                 dist.broadcast(p.data, 0)
+        # ... but independent exploration noise per rank (its own env shard)
+        self.sample_gen = sampling_generator(seed, self.device)
         multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
         self.use_graphs = (not multi) if use_graphs is None else bool(use_graphs) and not multi
         # fused Adam on the GPU: one kernel for all parameters instead of ~4
@@ -286,7 +339,9 @@ class PPO:
         self._graph = None
         self._graph_warm = 0
         self.n_steps, self.batch_size, self.n_epochs = int(n_steps), int(batch_size), int(n_epochs)
+        # clip_range may be an SB3-style schedule: f(progress_remaining) -> value
         self.gamma, self.gae_lambda, self.clip_range = gamma, gae_lambda, clip_range
+        self._progress = 1.0
         self.ent_coef, self.vf_coef, self.max_grad_norm = ent_coef, vf_coef, max_grad_norm
         self.normalize_advantage = normalize_advantage
         # the loss head runs as the fused HIP kernels of salp_ppo_loss for the
@@ -296,6 +351,8 @@ class PPO:
         self.verbose = verbose
         self.reset_nonfinite = reset_nonfinite
         self._nonfinite = torch.zeros((), dtype=torch.int64, device=self.device)
+        # finished-episode statistics of the current collection (device, sync-free)
+        self._ep_stats = torch.zeros(2, dtype=torch.float64, device=self.device)
         self.gen = g
         self.buf = RolloutBuffer(self.n_steps, self.n_envs, self.obs_dim, self.act_dim, self.device)
         self.low = torch.tensor([0.0, 0.0, -1.0], device=self.device)
@@ -305,25 +362,38 @@ class PPO:
         self.num_timesteps = 0
         self.logger = {}
         self.timing = {"collect_s": 0.0, "gae_s": 0.0, "train_s": 0.0}
+        self.history = []   # per iteration: losses, finished-episode mean return, diverged envs
 
     # ---------------------------------------------------------- rollout
     def collect_rollouts(self):
+        """n_steps lock-step env-steps into the buffer, then GAE.  Returns the
+        HIP events (start, before GAE, after GAE) on the current stream, so
+        the split of the GPU timeline is attributed to the right phase."""
         b, sim, pol = self.buf, self.sim, self.policy
+        stream = torch.cuda.current_stream(self.device)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ev[0].record(stream)
         if self._obs is None:
             self._obs = sim.reset()
+        self._ep_stats.zero_()
         for t in range(self.n_steps):
             obs = self._obs
-            a, v, lp = pol.act(obs)
+            a, v, lp = pol.act(obs, generator=self.sample_gen)
             r = sim.step(torch.clamp(a, self.low, self.high), auto_reset=True, want_terminal_obs=True)
             rew = r.reward.float()
+            bad = None
             if self.reset_nonfinite:
-                rew = self._reset_nonfinite(r, rew)
+                rew, bad = self._reset_diverged(r, rew)
             # no host sync in the loop: the bootstrap value is computed for every
             # env and selected where the episode was truncated, not terminated
-            trunc_only = r.truncated & ~r.terminated
             with torch.no_grad():
                 tv = pol.value(r.terminal_obs)
-            rew = torch.where(trunc_only, rew + self.gamma * tv, rew)
+            rew = timeout_bootstrap(rew, r.terminated, r.truncated, tv, self.gamma)
+            done = (r.terminated | r.truncated)
+            ended = done if bad is None else done & ~bad    # episodes that ended by the task's rules
+            ep_ret = r.info[:, _EP_RETURN]
+            self._ep_stats += torch.stack([torch.where(ended, ep_ret, torch.zeros_like(ep_ret)).sum(),
+                                           ended.sum().double()])
             b.obs[t].copy_(obs)
             b.actions[t].copy_(a)
             b.rewards[t].copy_(rew)
@@ -331,34 +401,41 @@ class PPO:
             b.values[t].copy_(v)
             b.log_probs[t].copy_(lp)
             self._obs = r.obs
-            self._episode_starts = (r.terminated | r.truncated).float()
+            self._episode_starts = done.float()
         with torch.no_grad():
             last_values = pol.value(self._obs).contiguous()
-        t0 = time.perf_counter()
+        ev[1].record(stream)
         compute_gae(b.rewards, b.values, b.episode_starts, last_values, self._episode_starts.contiguous(),
                     self.gamma, self.gae_lambda, b.advantages, b.returns)
-        return t0
+        ev[2].record(stream)
+        return ev
 
-    def _reset_nonfinite(self, r, rew):
+    def _reset_diverged(self, r, rew):
         """The reference integrator diverges for some actions (jet_time < dt,
         tests/test_gpu_parity.py::test_reference_blowup_is_reproduced) and its
-        env then returns NaN observations until the 500-cycle timeout.  A
-        learner cannot consume those: such envs are reset on the spot and the
-        step is recorded as a truncation with reward 0 and no bootstrap.
-        Sync-free: the masked reset is a no-op where the mask is all zero."""
-        bad = ~torch.isfinite(r.obs).all(1) | ~torch.isfinite(rew)
+        env then returns huge, later NaN, observations and rewards until the
+        500-cycle timeout.  A learner cannot consume those: envs flagged by
+        :func:`diverged_mask` are reset on the spot and the step is recorded as
+        a termination with reward 0 (no bootstrap from a diverged state).
+        Sync-free: the masked reset is a no-op where the mask is all zero.
+        Returns (reward, diverged mask)."""
+        bad = diverged_mask(r.obs, rew)
         self._nonfinite = self._nonfinite + bad.sum()
         fresh = self.sim.reset(mask=bad)
         col = bad.unsqueeze(1)
         r.obs.copy_(torch.where(col, fresh, r.obs))
         r.truncated |= bad
         r.terminated |= bad     # terminal: no gamma * V(terminal_obs) bootstrap
-        return torch.where(bad, torch.zeros_like(rew), rew)
+        return torch.where(bad, torch.zeros_like(rew), rew), bad
 
     @property
     def nonfinite_resets(self):
         """Envs reset because their state diverged (host int; syncs)."""
         return int(self._nonfinite)
+
+    def _clip(self):
+        c = self.clip_range
+        return float(c(self._progress)) if callable(c) else float(c)
 
     # ----------------------------------------------------------- update
     def _minibatch(self, idx, acc):
@@ -371,7 +448,7 @@ class PPO:
         norm = self.normalize_advantage and idx.numel() > 1
         if self.fused_loss:
             mean = pol.action_net(pol.pi_net(obs))
-            loss, stats = ppo_loss(mean, pol.log_std, pol.value(obs), act, *rows, self.clip_range, self.ent_coef,
+            loss, stats = ppo_loss(mean, pol.log_std, pol.value(obs), act, *rows, self._clip(), self.ent_coef,
                                    self.vf_coef, norm)
         else:   # any policy exposing evaluate(obs, actions) -> (value, log_prob, entropy)
             v, lp, ent = pol.evaluate(obs, act)
@@ -379,11 +456,12 @@ class PPO:
             if norm:
                 adv = (adv - adv.mean()) / (adv.std() + 1e-8)
             ratio = torch.exp(lp - old_lp)
-            pg = -torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - self.clip_range, 1 + self.clip_range)).mean()
+            cr = self._clip()
+            pg = -torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - cr, 1 + cr)).mean()
             vf = torch.nn.functional.mse_loss(ret, v)
             ent_loss = -ent.mean()
             loss = pg + self.ent_coef * ent_loss + self.vf_coef * vf
-            clip = ((ratio - 1).abs() > self.clip_range).float().mean()
+            clip = ((ratio - 1).abs() > cr).float().mean()
             stats = torch.stack([pg.detach(), vf.detach(), -ent_loss.detach(), clip.detach()])
         loss.backward()
         allreduce_gradients(list(pol.parameters()))
@@ -438,20 +516,32 @@ class PPO:
         return dict(zip(("pg_loss", "vf_loss", "entropy", "clip_frac"), vals))
 
     def learn(self, total_timesteps, log_interval=1):
+        """Collect + GAE + update until ``total_timesteps`` env-steps.  The
+        phase timings come from HIP events on the stream (collection, GAE and
+        update are attributed where the GPU ran them); ``history`` gets one
+        row per iteration."""
         it = 0
+        start_steps = self.num_timesteps
+        stream = torch.cuda.current_stream(self.device)
         while self.num_timesteps < total_timesteps:
-            t0 = time.perf_counter()
-            tg = self.collect_rollouts()
-            torch.cuda.synchronize(self.device)
-            t1 = time.perf_counter()
+            done_frac = (self.num_timesteps - start_steps) / max(total_timesteps - start_steps, 1)
+            self._progress = 1.0 - done_frac
+            div0 = self._nonfinite.clone()
+            ev = self.collect_rollouts()
             self.logger = self.train()
-            torch.cuda.synchronize(self.device)
-            t2 = time.perf_counter()
-            self.timing["collect_s"] += tg - t0
-            self.timing["gae_s"] += t1 - tg
-            self.timing["train_s"] += t2 - t1
+            end = torch.cuda.Event(enable_timing=True)
+            end.record(stream)
+            end.synchronize()
+            self.timing["collect_s"] += ev[0].elapsed_time(ev[1]) / 1e3
+            self.timing["gae_s"] += ev[1].elapsed_time(ev[2]) / 1e3
+            self.timing["train_s"] += ev[2].elapsed_time(end) / 1e3
             self.num_timesteps += self.n_steps * self.n_envs
             it += 1
+            ret_sum, n_ep = self._ep_stats.tolist()
+            row = {"iteration": len(self.history) + 1, "timesteps": self.num_timesteps, **self.logger,
+                   "episodes": int(n_ep), "ep_return_mean": ret_sum / n_ep if n_ep else None,
+                   "diverged_envs": int(self._nonfinite - div0)}
+            self.history.append(row)
             if self.verbose and it % log_interval == 0:
-                print({"iteration": it, "timesteps": self.num_timesteps, **self.logger}, flush=True)
+                print(row, flush=True)
         return self

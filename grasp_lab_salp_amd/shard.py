@@ -10,7 +10,7 @@ the CPU tests).
 import torch
 import torch.distributed as dist
 
-__all__ = ["env_id_offset", "reduce_run"]
+__all__ = ["env_id_offset", "reduce_run", "reduce_sums"]
 
 
 def env_id_offset(rank, n_envs_per_rank):
@@ -33,3 +33,14 @@ def reduce_run(elapsed_s, env_steps, kernel_ms, lockstep_rate, device=None):
     dist.all_reduce(mx, op=dist.ReduceOp.MAX)
     dist.all_reduce(sm, op=dist.ReduceOp.SUM)
     return mx[0].item(), sm[1].item(), mx[2].item(), sm[3].item()
+
+
+def reduce_sums(values, device=None):
+    """SUM of per-rank counters (e.g. diverged envs) over ranks; the inputs
+    themselves without an initialised process group.  Returns python ints."""
+    vals = [int(v) for v in values]
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return vals
+    t = torch.tensor(vals, dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [int(x) for x in t.tolist()]

@@ -100,3 +100,83 @@ def test_graphed_update_equals_eager_update():
         env.close()
     # same data and steps; only Adam's capturable (tensor-step) arithmetic differs by rounding
     assert torch.allclose(params[0], params[1], rtol=1e-4, atol=1e-6)
+
+
+def _flat(model):
+    return torch.cat([p.detach().reshape(-1) for p in model.policy.parameters()]).clone()
+
+
+def test_fused_and_unfused_train_agree_on_the_same_buffer():
+    """One PPO.train() with the fused HIP loss head and one with the torch
+    loss, from the same weights on the same rollout buffer and minibatch order:
+    parameters agree to float32 rounding (whole-update check)."""
+    from grasp_lab_salp_amd.ppo import PPO
+    from grasp_lab_salp_amd.vec_env import SalpVecEnv
+    env = SalpVecEnv(256, seed=4, infos=False)
+    a = PPO("MlpPolicy", env, n_steps=4, batch_size=256, n_epochs=2, seed=2, use_graphs=False, fused_loss=True)
+    b = PPO("MlpPolicy", env, n_steps=4, batch_size=256, n_epochs=2, seed=2, use_graphs=False, fused_loss=False)
+    b.policy.load_state_dict(a.policy.state_dict())
+    # plain SGD on both: Adam's per-parameter normalisation would turn float32
+    # noise in near-zero gradients into +-lr steps and hide the comparison
+    a.opt = torch.optim.SGD(a.policy.parameters(), lr=1e-2)
+    b.opt = torch.optim.SGD(b.policy.parameters(), lr=1e-2)
+    a.collect_rollouts()
+    for k in ("obs", "actions", "rewards", "episode_starts", "values", "log_probs", "advantages", "returns"):
+        getattr(b.buf, k).copy_(getattr(a.buf, k))
+    b.gen.set_state(a.gen.get_state())
+    la, lb = a.train(), b.train()
+    pa, pb = _flat(a), _flat(b)
+    assert torch.allclose(pa, pb, rtol=1e-4, atol=1e-6), (pa - pb).abs().max()
+    for k in la:
+        assert abs(la[k] - lb[k]) <= 1e-4 * max(1.0, abs(lb[k])), (k, la[k], lb[k])
+    env.close()
+
+
+def test_diverged_envs_are_reset_without_bootstrap():
+    """The reference's blow-up action (test_reference_blowup_is_reproduced)
+    on 4 of 8 envs: the learner's guard resets exactly those envs, records the
+    step as a termination (no timeout bootstrap) with reward 0, and the next
+    observation is the fresh reset observation."""
+    from grasp_lab_salp_amd._abi import FIELD
+    from grasp_lab_salp_amd.ppo import PPO
+    from grasp_lab_salp_amd.vec_env import SalpVecEnv
+    env = SalpVecEnv(8, seed=0, infos=False)
+    model = PPO("MlpPolicy", env, n_steps=2, batch_size=16, n_epochs=1, seed=0)
+    sim = model.sim
+    sim.reset()
+    act = torch.full((8, 3), 0.5, device="cuda")
+    act[:4] = torch.tensor([0.0904393, 0.06936062, -0.76570743], device="cuda")
+    r = sim.step(act, auto_reset=True, want_terminal_obs=True)
+    raw = r.reward.float().clone()
+    rew, bad = model._reset_diverged(r, r.reward.float())
+    assert bad.tolist() == [True] * 4 + [False] * 4
+    assert model.nonfinite_resets == 4
+    assert torch.isfinite(r.obs).all() and torch.isfinite(rew).all()
+    assert torch.equal(rew[:4], torch.zeros(4, device="cuda")) and torch.equal(rew[4:], raw[4:])
+    assert r.terminated[:4].all() and r.truncated[:4].all()
+    st = sim.get_state()
+    assert (st[FIELD["ep_len"], :4] == 0).all()
+    assert torch.isfinite(st[FIELD["v0"]:FIELD["ang2"] + 1, :4]).all()
+
+
+def test_timeout_bootstrap_in_collection():
+    """max_cycles = 1: every env-step ends by the time limit, so every buffer
+    reward is the env reward + gamma * V(terminal_obs) (SB3 collect_rollouts)."""
+    from grasp_lab_salp_amd._abi import default_params
+    from grasp_lab_salp_amd.ppo import timeout_bootstrap, PPO
+    from grasp_lab_salp_amd.vec_env import SalpVecEnv
+    p = default_params(max_cycles=1)
+    env = SalpVecEnv(64, params=p, seed=6, infos=False)
+    model = PPO("MlpPolicy", env, n_steps=1, batch_size=64, n_epochs=1, seed=3)
+    model.collect_rollouts()
+    twin = SalpVecEnv(64, params=p, seed=6, infos=False)
+    twin.sim.reset()
+    r = twin.sim.step(torch.clamp(model.buf.actions[0], model.low, model.high), auto_reset=True,
+                      want_terminal_obs=True)
+    assert r.truncated.all()
+    with torch.no_grad():
+        tv = model.policy.value(r.terminal_obs)
+    want = timeout_bootstrap(r.reward.float(), r.terminated, r.truncated, tv, model.gamma)
+    ok = ~r.terminated
+    assert torch.equal(model.buf.rewards[0][ok], want[ok])
+    assert not torch.equal(model.buf.rewards[0][ok], r.reward.float()[ok])

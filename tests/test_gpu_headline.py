@@ -1,0 +1,165 @@
+"""The HIP path at BASELINE.json's headline sizes (configs[2] and configs[3]).
+
+configs[2]: 65 536 envs, random-action rollout on one MI355X (the bench
+workload, src/salp_robot_env.py:196-299 per env-step).  configs[3]: 524 288
+envs sharded 8 ways, i.e. a 65 536-env handle whose global env ids start at
+rank * 65 536 (here the last rank, 7 * 65 536).
+
+* split invariance at full size: one 8 245-tick launch == the same ticks cut
+  into 85 launches of 97 (state, steps_done and rollout buffers, bit for bit);
+* the headline rollout against the C oracle (oracle/salp_oracle.c, pinned to
+  the reference by tests/test_oracle_golden.py) on blocks of env ids spread
+  over the 65 536, buffers included;
+* the lock-step kernel on ALL 65 536 envs against the OpenMP oracle;
+* the config-4 shard (global ids up to 2^19 - 1, plus a block across 2^32 for
+  the Philox counter's high word) against the oracle at the same global ids.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from grasp_lab_salp_amd._abi import FIELD, default_params
+from grasp_lab_salp_amd.batched_env import BatchedSalpEnv
+from oracle import oracle as orc
+from test_gpu_parity import assert_state_equal, philox_action
+
+pytestmark = pytest.mark.gpu
+
+N = 65536
+SEED = 17
+
+
+def _threads():
+    return int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+
+
+def _cpu(t):
+    return t.detach().cpu().numpy()
+
+
+def _bits(t):
+    t = t.contiguous()
+    if t.dtype == torch.float64:
+        return t.view(torch.int64)
+    if t.dtype == torch.float32:
+        return t.view(torch.int32)
+    return t
+
+
+def _bits_equal(x, y):
+    return x.shape == y.shape and torch.equal(_bits(x), _bits(y))
+
+
+def _buffers(cap, n, dev="cuda"):
+    return {"obs": torch.full((cap, n, 10), -7.0, device=dev),
+            "actions": torch.full((cap, n, 3), -7.0, device=dev),
+            "rewards": torch.full((cap, n), -7.0, device=dev),
+            "dones": torch.full((cap, n), 255, dtype=torch.uint8, device=dev)}
+
+
+def test_headline_rollout_is_split_invariant_at_65536():
+    """One launch of 85 chunks of 97 ticks == 85 launches of one 97-tick chunk
+    (env-steps end and start only at chunk boundaries, so both runs see the
+    same boundaries).  DESIGN.md §4 'Full-size properties' cites this test."""
+    p = default_params()
+    chunk, launches = 97, 85
+    a = BatchedSalpEnv(N, params=p, seed=SEED)
+    b = BatchedSalpEnv(N, params=p, seed=SEED)
+    ba, bb = _buffers(32, N), _buffers(32, N)
+    sa = torch.zeros(N, dtype=torch.int64, device="cuda")
+    sb = torch.zeros(N, dtype=torch.int64, device="cuda")
+    a.rollout(chunk * launches, buffers=ba, steps_done=sa, chunk=chunk)
+    for _ in range(launches):
+        b.rollout(chunk, buffers=bb, steps_done=sb, chunk=chunk)
+    torch.cuda.synchronize()
+    assert int(sa.min()) >= 3, "every env should complete a few env-steps in 8 245 ticks"
+    assert int(sa.max()) < 32, "the 32-slot buffers must not wrap in this test"
+    assert torch.equal(sa, sb)
+    assert _bits_equal(a.get_state(), b.get_state())
+    for k in ba:
+        assert _bits_equal(ba[k], bb[k]), k
+    # slots past steps_done are untouched, slots below are written
+    slot = torch.arange(32, device="cuda").unsqueeze(1)
+    written = slot < sa.unsqueeze(0)
+    assert bool((ba["dones"][written] != 255).all()) and bool((ba["dones"][~written] == 255).all())
+    # every completed env-step was counted
+    assert int(sa.sum()) == int(written.sum())
+
+
+def _oracle_rollout(seed, start, n, steps, env_offset_base=0):
+    """The chained rollout per env == env-steps with Philox actions keyed by
+    (seed, global id, step count) and auto-reset: the oracle step by step."""
+    o = orc.Oracle(default_params(), n, seed=seed, env_offset=env_offset_base + start)
+    o.reset()
+    outs, acts = [], []
+    for _ in range(steps):
+        act = np.zeros((n, 3), np.float32)
+        sc = o.state[FIELD["step_count"]]
+        for i in range(n):
+            act[i] = philox_action(seed, env_offset_base + start + i, int(sc[i]))
+        outs.append(o.step(act, auto_reset=True))
+        acts.append(act)
+    return o, acts, outs
+
+
+def _check_blocks(env, bufs, done, steps, blocks, seed, base=0):
+    g = _cpu(env.get_state())
+    assert int(done.min()) == steps and int(done.max()) == steps
+    for start, n in blocks:
+        o, acts, outs = _oracle_rollout(seed, start, n, steps, base)
+        sl = slice(start, start + n)
+        assert_state_equal(g[:, sl], o.state, f"block {base + start}")
+        for t in range(steps):
+            assert np.array_equal(_cpu(bufs["actions"][t, sl]), acts[t]), (start, t)
+            assert np.array_equal(_cpu(bufs["obs"][t, sl]), outs[t]["terminal_obs"], equal_nan=True), (start, t)
+            assert np.array_equal(_cpu(bufs["rewards"][t, sl]), outs[t]["reward"].astype(np.float32),
+                                  equal_nan=True), (start, t)
+            dn = outs[t]["terminated"] | (outs[t]["truncated"] << 1)
+            assert np.array_equal(_cpu(bufs["dones"][t, sl]), dn), (start, t)
+
+
+def test_headline_rollout_matches_oracle_on_blocks():
+    """configs[2]: 65 536 envs, 3 env-steps each through k_rollout (buffers
+    filled), checked against the oracle on 4 blocks of env ids."""
+    steps = 3
+    env = BatchedSalpEnv(N, params=default_params(), seed=SEED)
+    bufs = _buffers(steps, N)
+    done = torch.zeros(N, dtype=torch.int64, device="cuda")
+    env.rollout(6000, buffers=bufs, steps_done=done, max_steps=steps)
+    torch.cuda.synchronize()
+    _check_blocks(env, bufs, done, steps, [(0, 256), (20000, 256), (45311, 256), (N - 256, 256)], SEED)
+
+
+def test_headline_lockstep_all_envs_match_openmp_oracle():
+    """k_step_random on every one of the 65 536 envs, 2 env-steps, against
+    the whole-batch OpenMP oracle (bit for bit: state and reward sums)."""
+    p = default_params()
+    env = BatchedSalpEnv(N, params=p, seed=SEED)
+    rs = env.step_random(2)
+    o = orc.Oracle(p, N, seed=SEED)
+    o.reset()
+    rs_o, ticks = o.step_random(2, threads=_threads())
+    assert ticks > 0
+    assert np.array_equal(_cpu(rs), rs_o, equal_nan=True)
+    assert_state_equal(env.get_state(), o.state, "lock-step 65536")
+
+
+@pytest.mark.parametrize("base", [7 * N, (1 << 32) - N // 2])
+def test_config4_shard_matches_oracle_at_its_global_ids(base):
+    """configs[3]: the last of 8 shards (global ids 458 752 .. 524 287), and a
+    shard whose ids cross 2^32 (Philox counter high word), 2 env-steps each;
+    blocks checked against the oracle keyed by the same global ids."""
+    steps = 2
+    env = BatchedSalpEnv(N, params=default_params(), seed=SEED, env_id_offset=base)
+    bufs = _buffers(steps, N)
+    done = torch.zeros(N, dtype=torch.int64, device="cuda")
+    env.rollout(4000, buffers=bufs, steps_done=done, max_steps=steps)
+    torch.cuda.synchronize()
+    _check_blocks(env, bufs, done, steps, [(0, 128), (N // 2 - 64, 128), (N - 128, 128)], SEED, base)
+    # the shard's envs are the same envs as in a smaller handle at those ids
+    part = BatchedSalpEnv(256, params=default_params(), seed=SEED, env_id_offset=base + 1000)
+    dp = torch.zeros(256, dtype=torch.int64, device="cuda")
+    part.rollout(4000, steps_done=dp, max_steps=steps)
+    assert _bits_equal(part.get_state(), env.get_state()[:, 1000:1256].contiguous())

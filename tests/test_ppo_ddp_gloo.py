@@ -8,7 +8,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from grasp_lab_salp_amd.ppo import ActorCritic, allreduce_gradients
+from grasp_lab_salp_amd.ppo import ActorCritic, allreduce_gradients, sampling_generator
 
 
 def _port():
@@ -47,8 +47,14 @@ def _worker(rank, world, port, q):
     flat = torch.cat([p.detach().reshape(-1) for p in pol.parameters()])
     parts = [torch.empty_like(flat) for _ in range(world)]
     dist.all_gather(parts, flat)
+    # exploration noise: PPO seeds every rank with the same seed (identical
+    # policies), the sampling generator must still differ per rank
+    torch.manual_seed(0)
+    a, _, _ = pol.act(torch.zeros(16, 10), generator=sampling_generator(0, "cpu"))
+    acts = [torch.empty_like(a) for _ in range(world)]
+    dist.all_gather(acts, a)
     if rank == 0:
-        q.put(torch.stack(parts).numpy())
+        q.put((torch.stack(parts).numpy(), torch.stack(acts).numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -60,11 +66,12 @@ def test_two_ranks_stay_identical_and_match_averaged_step():
     ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    got = q.get(timeout=300)
+    got, acts = q.get(timeout=300)
     for p in ps:
         p.join(timeout=60)
     assert all(p.exitcode == 0 for p in ps)
     assert (got[0] == got[1]).all()
+    assert not (acts[0] == acts[1]).any(), "ranks drew the same exploration noise"
     # single process: same init (rank 0's), gradient = mean of both ranks' grads
     torch.manual_seed(0)
     pol = ActorCritic(10, 3)

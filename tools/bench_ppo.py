@@ -1,12 +1,22 @@
 """BASELINE.json config 5: PPO on 32 768 envs per GPU with the HIP GAE scan.
 
-    python tools/bench_ppo.py [--n-envs 32768] [--n-steps 32] [--iters 2]
+    python tools/bench_ppo.py [--n-envs 32768] [--n-steps 32] [--iters 2] [--trend-iters 0]
     python -m torch.distributed.run --nproc-per-node N tools/bench_ppo.py ...
 
 Prints one JSON line: full-iteration env-steps/s (collection + GAE + update,
-max time over ranks), the split, and the GAE kernel alone against the HBM
-roofline (12 B read + 8 B written per (step, env), HIP events on the stream
-it runs on).
+max time over ranks), the split (HIP events on the stream: collection, GAE and
+update each where the GPU ran them), the per-iteration history (losses, mean
+return of the episodes that ended, envs reset by the divergence guard), and the
+GAE kernel alone against the HBM roofline (12 B read + 8 B written per (step,
+env)).  --trend-iters K first runs K untimed iterations and reports their
+history (a learning trend), then the timed ones.
+
+The reference's RecurrentPPO uses n_steps 2048, batch 64 with 4 envs
+(src/train_robot_recurrent_ppo.py:91-93): 128 minibatches per epoch.  At
+32 768 envs the buffer of n_steps 2048 (MLP policy: obs, actions, rewards,
+starts, values, log-probs, advantages, returns = 19 floats per (step, env),
+5.1 GB) fits in HBM easily; batch 64 would mean 1 048 576 minibatches per
+epoch, so the batch is scaled with the env count (default 32 768).
 """
 import argparse
 import json
@@ -55,6 +65,7 @@ def main():
     ap.add_argument("--n-epochs", type=int, default=10)
     ap.add_argument("--iters", type=int, default=2)
     ap.add_argument("--gae-steps", type=int, default=2048)
+    ap.add_argument("--trend-iters", type=int, default=0)
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -67,7 +78,8 @@ def main():
     from grasp_lab_salp_amd.vec_env import SalpVecEnv
     env = SalpVecEnv(a.n_envs, seed=0, env_id_offset=env_id_offset(rank, a.n_envs), infos=False)
     model = PPO("MlpPolicy", env, n_steps=a.n_steps, batch_size=a.batch_size, n_epochs=a.n_epochs, seed=0)
-    model.learn(a.n_steps * a.n_envs)   # warm-up iteration
+    model.learn(max(1, a.trend_iters) * a.n_steps * a.n_envs)   # warm-up (+ trend) iterations
+    trend = list(model.history)
     for k in model.timing:
         model.timing[k] = 0.0
     torch.cuda.synchronize()
@@ -75,6 +87,7 @@ def main():
         dist.barrier()
     t0 = time.perf_counter()
     model.num_timesteps = 0
+    h0 = len(model.history)
     model.learn(a.iters * a.n_steps * a.n_envs)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
@@ -84,6 +97,8 @@ def main():
                "unit": "env-steps/s", "n_gpus": world, "n_envs_per_gpu": a.n_envs, "n_steps": a.n_steps,
                "batch_size": a.batch_size, "n_epochs": a.n_epochs, "iters": a.iters,
                "timing_s": model.timing, "losses": model.logger,
+               "history": model.history[h0:], "trend": trend if a.trend_iters else None,
+               "diverged_envs_reset": model.nonfinite_resets,
                "gae_kernel": gae_roofline(a.gae_steps, a.n_envs)}
         print(json.dumps(res), flush=True)
     if world > 1:
