@@ -263,3 +263,34 @@ def test_timeout_and_zero_tick_cycles():
     assert_state_equal(env.get_state(), o.state, "timeout")
     assert np.all(_cpu(env.field("cycle")) == 500)
     assert np.all(_cpu(env.field("time")) == 0)
+
+
+def test_float32_shape_carried_across_cycles():
+    """A cycle that ends while REFILL still holds the float32 contracted body
+    (contraction ~0, no coast: jet + coast < 0) followed by a cycle that starts
+    in a different float32 shape: the first tick has both volumes float32 but
+    V != prev V, the one case where jet_rates' float32 arm differs from its
+    float64 arm (r2 experiment log).  Mixed with ordinary lanes in every wave;
+    device == oracle bit for bit."""
+    n = 256
+    env, o = make_pair(n, seed=8)
+    o.reset()
+    rng = np.random.default_rng(3)
+    a1 = random_actions(rng, n)
+    a2 = random_actions(rng, n)
+    sel = np.arange(n) % 2 == 0
+    a1[sel, 0] = 0.0
+    a1[sel, 1] = 0.0
+    a1[sel, 2] = np.linspace(-1, 1, sel.sum())
+    a2[sel, 0] = 0.05
+    a2[sel, 1] = 0.0
+    a2[sel, 2] = -np.linspace(-1, 1, sel.sum())
+    for t, a in enumerate((a1, a2, random_actions(rng, n))):
+        r = env.step(torch.tensor(a), auto_reset=True)
+        ro = o.step(a, auto_reset=True)
+        assert np.array_equal(_cpu(r.obs), ro["obs"], equal_nan=True), t
+        assert np.array_equal(_cpu(r.reward), ro["reward"], equal_nan=True), t
+        assert_state_equal(env.get_state(), o.state, f"step {t}")
+        if t == 0:   # (almost all) even lanes end the cycle in the float32 REFILL shape
+            in32 = (o.state[FIELD["geom32"], sel] == 1) & (o.state[FIELD["phase"], sel] == 0)
+            assert in32.mean() > 0.9
