@@ -194,7 +194,14 @@ SM_QUAL int sm_rem_pio2(double x, double* y0, double* y1) {
     }
     *y0 = y;
     *y1 = (r - y) - w;
-    return (int)fn;
+    /* The quadrant fn mod 4, exactly, for every fn: (int)fn is undefined in C
+     * (and saturates on the GPU) once |fn| >= 2^31, which a diverged env's
+     * angle reaches (UBSan, tools/sanitize).  Callers only use n & 3; for
+     * |fn| < 2^31 this is exactly (int)fn & 3.  (Beyond |x| = 2^20 pi/2 the
+     * medium-case reduction is inexact, as in fdlibm's medium branch; such
+     * angles only occur in envs whose state already diverged.) */
+    const double q = fn - 4.0 * floor(fn * 0.25);
+    return q == q ? (int)q : 0;
 }
 SM_QUAL void sm_sincos_p(double x, double* s_out, double* c_out, SmPoly K) {
     int32_t ix = sm_hi(x) & 0x7fffffff;
