@@ -15,7 +15,8 @@ kernels): the multi-rank plumbing test of tests/test_bench_launcher.py.
 Workload (BASELINE.json configs[2]): 65 536 envs per GPU, canonical robot and
 env of src/train_robot.py:11-21, synthetic random actions U(action box) from
 on-device Philox, SB3-style auto-reset, rollout-buffer fill (obs, action,
-reward, done per env-step).  One bench "step" = one launch of the chained
+reward, done and the observation the action was taken on, per env-step).  One
+bench "step" = one launch of the chained
 rollout kernel in which every env runs --tick-budget physics ticks (dt 0.01 s)
 and completes as many env-steps (breathing cycles) as fit.  value = env-steps
 completed by all ranks / wall time (max over ranks).  Envs shard by global id
@@ -46,7 +47,9 @@ FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X fp64 vector spec (half the 157.3 TF fp32 
 # persistent per-env state an env-step reads and writes.  Here S = the 102
 # fields before the randomisation block (the plain path never touches those).
 STATE_BYTES = FIELD["cd"] * 8
-STEP_OUT_BYTES = 10 * 4 + 3 * 4 + 4 + 1   # obs + action + reward(f32) + done per env-step
+# per env-step into the rollout buffer: obs before and after the step, action,
+# reward (f32) and done
+STEP_OUT_BYTES = 2 * 10 * 4 + 3 * 4 + 4 + 1
 BYTES_PER_ENV_STEP = 2 * STATE_BYTES + STEP_OUT_BYTES
 # Algorithmic fp64 work of one physics tick ("F_TICK"): the
 # reference's operations (src/robot.py:789-875, src/dynamics.py, src/geometry.py)
@@ -242,6 +245,7 @@ def main(argv=None):
                          device=dev.index)
     cap = a.capacity
     bufs = {"obs": torch.zeros((cap, n, env.obs_dim), dtype=torch.float32, device=dev),
+            "obs_before": torch.zeros((cap, n, env.obs_dim), dtype=torch.float32, device=dev),
             "actions": torch.zeros((cap, n, 3), dtype=torch.float32, device=dev),
             "rewards": torch.zeros((cap, n), dtype=torch.float32, device=dev),
             "dones": torch.zeros((cap, n), dtype=torch.uint8, device=dev)}
@@ -333,7 +337,7 @@ def main(argv=None):
                      "traffic_source": prof[0] if prof else None,
                      "bytes_per_launch": bytes_launch,
                      "bytes_per_env_step": BYTES_PER_ENV_STEP,
-                     "note": "algorithmic bytes = env-steps per launch x (2 x 816 B state + 57 B outputs) "
+                     "note": "algorithmic bytes = env-steps per launch x (2 x 816 B state + 97 B outputs) "
                              "(SURVEY 8(d)); the kernel is fp64-VALU bound (see roofline_valu)"},
         "lockstep_env_steps_per_sec": lock_total,
         "divergence": {"diverged_envs_at_end": diverged_total, "envs": n * world,

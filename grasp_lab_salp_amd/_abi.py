@@ -6,7 +6,7 @@ drift apart silently.
 """
 import ctypes
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_OBSTACLES = 4
 OBS_DIM_MAX = 6 + 2 * MAX_OBSTACLES
 

@@ -31,6 +31,7 @@ class SalpRolloutBuffers(ctypes.Structure):
         ("max_steps", ctypes.c_int64),
         ("chunk", ctypes.c_int32),
         ("reserved", ctypes.c_int32),
+        ("obs_before", ctypes.c_void_p),
     ]
 
 
@@ -58,6 +59,7 @@ SIGNATURES = {
     "salp_step": (ctypes.c_int, [_H, _V, _V, _V, _V, _V, ctypes.c_int, _V, _V, _V]),
     "salp_rollout": (ctypes.c_int, [_H, ctypes.c_int64, ctypes.POINTER(SalpRolloutBuffers), _V]),
     "salp_step_random": (ctypes.c_int, [_H, ctypes.c_int32, _V, _V]),
+    "salp_set_lockstep_order": (ctypes.c_int, [_H, ctypes.c_int]),
     "salp_robot_reset": (ctypes.c_int, [_H, _V, _V]),
     "salp_nozzle_set_angles": (ctypes.c_int, [_H, _V, _V]),
     "salp_nozzle_solve": (ctypes.c_int, [_H, _V, ctypes.c_int, _V]),

@@ -156,16 +156,25 @@ class BatchedSalpEnv:
         self._run(_lib.load().salp_step_random(self._h, int(n_steps), _ptr(rs), self._stream()))
         return rs
 
+    def set_lockstep_order(self, mode):
+        """Launch order of :meth:`step` / :meth:`step_random` (salp_set_lockstep_order):
+        1 = envs sorted by the predicted length of their next cycle, 0 = env
+        order, -1 = sorted when there are more envs than one wave per SIMD
+        holds (default).  Results are identical in every mode."""
+        self._check(_lib.load().salp_set_lockstep_order(self._h, int(mode)))
+
     def rollout(self, tick_budget, buffers=None, steps_done=None, max_steps=0, chunk=128):
         """Chained random-action rollout: each env runs ``tick_budget`` physics
         ticks, completing as many env-steps as fit (auto-reset).  ``buffers`` is
-        an optional dict of preallocated device tensors {obs [cap,n,obs_dim],
-        actions [cap,n,3], rewards [cap,n] f32, dones [cap,n] u8}; ``steps_done``
-        an int64 [n] tensor updated in place."""
+        an optional dict of preallocated device tensors {obs [cap,n,obs_dim]
+        (after the step), obs_before [cap,n,obs_dim] (the observation the
+        action was taken from, SB3's buffer obs), actions [cap,n,3], rewards
+        [cap,n] f32, dones [cap,n] u8}; ``steps_done`` an int64 [n] tensor
+        updated in place."""
         B = _lib.SalpRolloutBuffers()
         cap = 0
         if buffers:
-            for k in ("obs", "actions", "rewards", "dones"):
+            for k in ("obs", "obs_before", "actions", "rewards", "dones"):
                 t = buffers.get(k)
                 if t is not None:
                     if not t.is_contiguous() or t.device != self.device:

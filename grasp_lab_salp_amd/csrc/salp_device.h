@@ -37,6 +37,7 @@
 
 #define SD static __device__ __forceinline__
 #define SD_MEMBER __device__ __forceinline__
+#define SD_HOST_DEV static __host__ __device__ __forceinline__
 
 namespace salp {
 
@@ -73,6 +74,7 @@ struct Params {
     /* randomisation switches (SalpParams; salp_random.h) */
     int32_t rand_dyn, rand_dist, rand_act, rand_obs, latency;
     int64_t n;               /* envs on this device (SoA stride) */
+    int64_t cold_off;        /* first double of the env-major cold block (state layout below) */
     int64_t env_offset;      /* global id of env 0 */
     uint64_t seed;
 };
@@ -391,6 +393,71 @@ struct Hot {
     uint64_t env_id;
 };
 
+/* Fields store_hot writes (the tick's state); every other field is "cold":
+ * touched only at env-step boundaries.  RAND kernels also carry Hot::Rnd. */
+SD_HOST_DEV constexpr bool is_rnd(int f) {
+    return (f >= SALP_F_CD && f <= SALP_F_DTR) || (f >= SALP_F_AMF0 && f <= SALP_F_AMRF2) ||
+           (f >= SALP_F_AMT0 && f <= SALP_F_AMT2) || f == SALP_F_OUF0 || f == SALP_F_OUF1 ||
+           f == SALP_F_OUT2 || f == SALP_F_RNG_TICK;
+}
+template <bool RAND>
+SD_HOST_DEV constexpr bool is_hot(int f) {
+    return (f >= SALP_F_V0 && f <= SALP_F_ANG2) || (f >= SALP_F_LENGTH && f <= SALP_F_PVOL32) ||
+           (f >= SALP_F_CYCLE_TIME && f <= SALP_F_PHASE) || f == SALP_F_CONTR32 || f == SALP_F_TURN_TIME ||
+           (RAND && is_rnd(f));
+}
+/* One env's cold fields into registers with all loads in flight at once. */
+template <bool RAND>
+SD_HOST_DEV constexpr bool is_cached(int f) { return !is_hot<RAND>(f) && (RAND || f < SALP_F_CD); }
+
+/* ------------------------------------------------ state layout in HBM */
+/* The ABI's state is field-major, state[f * n + i] (salp_get_state and
+ * salp_set_state convert).  In HBM a handle keeps two regions:
+ *   rows:  every field but the cold ones, field-major [kLayout.n_rows][n]: a
+ *          wave's load of one field is one contiguous 512-B access (kernel
+ *          start and end; the RAND kernels' coefficient / OU fields);
+ *   block: the cold fields (is_cached<false>: read and written only at
+ *          env-step boundaries), env-major [n][COLD_SLOTS] from P.cold_off
+ *          (a multiple of 16 doubles): a lane that ends an env-step moves its
+ *          cold state as 16-B loads / stores within 4 whole 128-B lines,
+ *          instead of 55 scattered 8-B pieces of 55 rows.
+ * Every field has exactly one home (row or slot); field ids are compile-time
+ * constants at almost every access, so the lookups fold away. */
+#ifndef SALP_COLD_BLOCK
+#define SALP_COLD_BLOCK 1   /* 0: every field field-major (the round-1 layout; A/B builds) */
+#endif
+constexpr int COLD_SLOTS = 64;   /* 512 B per env: 4 lines, line-aligned */
+struct Layout {
+    int16_t row[SALP_NUM_FIELDS];    /* row of a field-major field, else -1 */
+    int16_t slot[SALP_NUM_FIELDS];   /* slot in the env's cold block, else -1 */
+    int n_rows, n_cold;
+};
+constexpr Layout make_layout() {
+    Layout L{};
+    int r = 0, c = 0;
+    for (int f = 0; f < SALP_NUM_FIELDS; ++f) {
+        if (SALP_COLD_BLOCK && is_cached<false>(f)) {
+            L.slot[f] = (int16_t)c++;
+            L.row[f] = -1;
+        } else {
+            L.row[f] = (int16_t)r++;
+            L.slot[f] = -1;
+        }
+    }
+    L.n_rows = r;
+    L.n_cold = c;
+    return L;
+}
+constexpr Layout kLayout = make_layout();
+static_assert(kLayout.n_cold <= COLD_SLOTS && (!SALP_COLD_BLOCK || kLayout.n_cold % 2 == 1),
+              "cold block: 16-B pairs + one tail");
+static_assert(kLayout.n_rows + kLayout.n_cold == SALP_NUM_FIELDS, "every field has one home");
+/* Offset of the cold block and total doubles of a handle's state (host). */
+SD_HOST_DEV constexpr int64_t layout_cold_off(int64_t n) { return ((int64_t)kLayout.n_rows * n + 15) / 16 * 16; }
+SD_HOST_DEV constexpr int64_t layout_doubles(int64_t n) {
+    return layout_cold_off(n) + (SALP_COLD_BLOCK ? (int64_t)COLD_SLOTS * n : 0);
+}
+
 /* State access.  The env-step functions below are templates over the state
  * they read and write: the struct-of-arrays buffer in HBM (double*), or a
  * register copy of one env's row (ColdRegs*, the rollout boundary) so that the
@@ -406,13 +473,16 @@ struct ColdRegs {
     double* g;   /* this env's column of the HBM state: g[f * n] */
     int64_t n;
 };
-SD double& sref(double* S, const Params& P, int64_t i, int f) { return S[(size_t)f * (size_t)P.n + (size_t)i]; }
-SD const double& sref(const double* S, const Params& P, int64_t i, int f) {
-    return S[(size_t)f * (size_t)P.n + (size_t)i];
+SD size_t state_index(const Params& P, int64_t i, int f) {
+    return kLayout.row[f] >= 0 ? (size_t)kLayout.row[f] * (size_t)P.n + (size_t)i
+                               : (size_t)P.cold_off + (size_t)i * COLD_SLOTS + (size_t)kLayout.slot[f];
 }
+SD double& sref(double* S, const Params& P, int64_t i, int f) { return S[state_index(P, i, f)]; }
+SD const double& sref(const double* S, const Params& P, int64_t i, int f) { return S[state_index(P, i, f)]; }
 template <bool RAND>
 SD double& sref(ColdRegs<RAND>* C, const Params&, int64_t, int f) {
-    return (!RAND && f >= SALP_F_CD) ? C->g[(size_t)f * (size_t)C->n] : C->v[f];
+    /* plain kernels: the randomisation fields live in rows, read in place */
+    return (!RAND && f >= SALP_F_CD) ? C->g[(size_t)kLayout.row[f] * (size_t)C->n] : C->v[f];
 }
 #define SF(f) sref(S, P, i, (f))
 
@@ -728,12 +798,8 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
 /* Nozzle.set_yaw_angle + Nozzle.solve_angles (src/robot.py:62-98).  yaw32:
  * the yaw is an np.float32 (env path, src/salp_robot_env.py:207), so np.cos /
  * np.sin run in float32; otherwise in float64. */
-template <class ST>
-SD void nozzle_solve(ST S, const Params& P, int64_t i, double yaw, bool yaw32) {
-    SF(SALP_F_PREV_YAW) = SF(SALP_F_YAW);
-    SF(SALP_F_YAW) = yaw;
-    SF(SALP_F_PREV_ANGLE1) = SF(SALP_F_ANGLE1);
-    SF(SALP_F_PREV_ANGLE2) = SF(SALP_F_ANGLE2);
+/* The angles solve_angles computes for a yaw (no state touched). */
+SD void nozzle_ik(double yaw, bool yaw32, double* an1_out, double* an2_out) {
     double sy, cy;
     if (yaw32) {
         float s, c;
@@ -764,8 +830,41 @@ SD void nozzle_solve(ST S, const Params& P, int64_t i, double yaw, bool yaw32) {
     }
     if (an1 <= -PI) an1 += 2 * PI;
     else if (an1 > PI) an1 -= 2 * PI;
+    *an1_out = an1;
+    *an2_out = an2;
+}
+template <class ST>
+SD void nozzle_solve(ST S, const Params& P, int64_t i, double yaw, bool yaw32) {
+    SF(SALP_F_PREV_YAW) = SF(SALP_F_YAW);
+    SF(SALP_F_YAW) = yaw;
+    SF(SALP_F_PREV_ANGLE1) = SF(SALP_F_ANGLE1);
+    SF(SALP_F_PREV_ANGLE2) = SF(SALP_F_ANGLE2);
+    double an1, an2;
+    nozzle_ik(yaw, yaw32, &an1, &an2);
     SF(SALP_F_ANGLE1) = an1;
     SF(SALP_F_ANGLE2) = an2;
+}
+
+/* Length in ticks of the breathing cycle an env-step with float32 action
+ * (a0, a1, a2) will run, from the current nozzle angles (which it updates in
+ * *ang1 / *ang2 for a following step): begin_step's control arithmetic
+ * (src/salp_robot_env.py:166-210, src/robot.py:544-592, 740-757) without
+ * touching the state.  ceil(total / dt) is within one tick of the
+ * accumulated-clock count; it only orders envs for the lock-step launch. */
+SD int predict_cycle_ticks(const Params& P, float a0, float a1, float a2, double* ang1, double* ang2) {
+    const float r0 = a0 * 0.06f, r1 = a1 * 10.0f, r2 = a2 * (float)(PI / 2);
+    double an1, an2;
+    nozzle_ik((double)r2, true, &an1, &an2);
+    const double turn = fabs(an1 - *ang1) / P.angle_speed + fabs(an2 - *ang2) / P.angle_speed;
+    *ang1 = an1;
+    *ang2 = an2;
+    const double c = (double)r0, sq = (double)sqf(r0);
+    const double refill = REFILL_C0 * sq + REFILL_C1 * c + REFILL_C2;
+    const double jet = PROPUL_C0 * sq + PROPUL_C1 * c + PROPUL_C2;
+    const double total = pymax(refill, turn) + jet + (double)r1;
+    if (!(total > 0.0)) return 0;
+    const double t = ceil(total / DT);
+    return t > 60000.0 ? 60000 : (int)t;
 }
 
 /* Nozzle.set_angles -> _nozzle_turn_time (src/robot.py:50-60, 173-185) */
@@ -1186,35 +1285,50 @@ SD void reset_env_philox(Hot& h, ST S, const Params& P, int64_t i, float* obs) {
 }
 
 /* ------------------------------------- rollout boundary: LDS + registers */
-/* Fields store_hot writes (the tick's state); every other field is "cold":
- * touched only at env-step boundaries.  RAND kernels also carry Hot::Rnd. */
-SD constexpr bool is_rnd(int f) {
-    return (f >= SALP_F_CD && f <= SALP_F_DTR) || (f >= SALP_F_AMF0 && f <= SALP_F_AMRF2) ||
-           (f >= SALP_F_AMT0 && f <= SALP_F_AMT2) || f == SALP_F_OUF0 || f == SALP_F_OUF1 ||
-           f == SALP_F_OUT2 || f == SALP_F_RNG_TICK;
-}
-template <bool RAND>
-SD constexpr bool is_hot(int f) {
-    return (f >= SALP_F_V0 && f <= SALP_F_ANG2) || (f >= SALP_F_LENGTH && f <= SALP_F_PVOL32) ||
-           (f >= SALP_F_CYCLE_TIME && f <= SALP_F_PHASE) || f == SALP_F_CONTR32 || f == SALP_F_TURN_TIME ||
-           (RAND && is_rnd(f));
-}
-/* One env's cold fields into registers with all loads in flight at once. */
-template <bool RAND>
-SD constexpr bool is_cached(int f) { return !is_hot<RAND>(f) && (RAND || f < SALP_F_CD); }
+/* One env's cold block as 16-B loads (all in flight at once), plus, in the
+ * RAND kernels, the randomisation fields they cache from their rows. */
 template <bool RAND>
 SD void load_cold(ColdRegs<RAND>& C, double* S, const Params& P, int64_t i) {
     C.g = S + i;
     C.n = P.n;
+    if (!SALP_COLD_BLOCK) {
 #pragma unroll
-    for (int f = 0; f < SALP_NUM_FIELDS; ++f)
-        if (is_cached<RAND>(f)) C.v[f] = S[(size_t)f * (size_t)P.n + (size_t)i];
+        for (int f = 0; f < SALP_NUM_FIELDS; ++f)
+            if (is_cached<RAND>(f)) C.v[f] = S[(size_t)f * (size_t)P.n + (size_t)i];
+        return;
+    }
+    const double2* blk = reinterpret_cast<const double2*>(S + P.cold_off + (size_t)i * COLD_SLOTS);
+    double v[kLayout.n_cold + 1];
+#pragma unroll
+    for (int k = 0; k < (kLayout.n_cold + 1) / 2; ++k) {
+        const double2 x = blk[k];
+        v[2 * k] = x.x;
+        v[2 * k + 1] = x.y;
+    }
+#pragma unroll
+    for (int f = 0; f < SALP_NUM_FIELDS; ++f) {
+        if (kLayout.slot[f] >= 0) C.v[f] = v[kLayout.slot[f]];
+        else if (is_cached<RAND>(f)) C.v[f] = S[(size_t)kLayout.row[f] * (size_t)P.n + (size_t)i];
+    }
 }
 template <bool RAND>
 SD void store_cold(const ColdRegs<RAND>& C, double* S, const Params& P, int64_t i) {
+    if (!SALP_COLD_BLOCK) {
 #pragma unroll
-    for (int f = 0; f < SALP_NUM_FIELDS; ++f)
-        if (is_cached<RAND>(f)) S[(size_t)f * (size_t)P.n + (size_t)i] = C.v[f];
+        for (int f = 0; f < SALP_NUM_FIELDS; ++f)
+            if (is_cached<RAND>(f)) S[(size_t)f * (size_t)P.n + (size_t)i] = C.v[f];
+        return;
+    }
+    double v[kLayout.n_cold + 1];
+#pragma unroll
+    for (int f = 0; f < SALP_NUM_FIELDS; ++f) {
+        if (kLayout.slot[f] >= 0) v[kLayout.slot[f]] = C.v[f];
+        else if (is_cached<RAND>(f)) S[(size_t)kLayout.row[f] * (size_t)P.n + (size_t)i] = C.v[f];
+    }
+    v[kLayout.n_cold] = 0.0;   /* padding slot of the last 16-B pair */
+    double2* blk = reinterpret_cast<double2*>(S + P.cold_off + (size_t)i * COLD_SLOTS);
+#pragma unroll
+    for (int k = 0; k < (kLayout.n_cold + 1) / 2; ++k) blk[k] = make_double2(v[2 * k], v[2 * k + 1]);
 }
 
 /* A lane's slot of a workgroup LDS array [SPILL_N][LANES]: the whole Hot
@@ -1294,6 +1408,8 @@ SD void calm_env(double* S, const Params& P, int64_t i, bool coefficients, bool 
 /* Robot / Nozzle / SalpRobotEnv constructors (src/robot.py:20-47, 261-412) */
 SD void construct_env(double* S, const Params& P, int64_t i) {
     for (int f = 0; f < SALP_NUM_FIELDS; ++f) SF(f) = 0.0;
+    if (SALP_COLD_BLOCK)
+        for (int k = kLayout.n_cold; k < COLD_SLOTS; ++k) S[P.cold_off + (size_t)i * COLD_SLOTS + k] = 0.0;
     const Core c0 = core(P.L0, P.W0, false);
     const double V = water_volume(P, c0, false);
     const Geo g = make_geo(P, c0, P.L0, P.W0, V, V, false, false, water_mass(P, V, false));

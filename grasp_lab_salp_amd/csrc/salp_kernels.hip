@@ -94,31 +94,61 @@ __global__ __launch_bounds__(kBlock) void k_reset_to(double* S, Params P, const 
         for (int k = 0; k < P.obs_dim; ++k) obs[(size_t)i * P.obs_dim + k] = o[k];
 }
 
+// The lock-step kernels run an env-step's prologue and epilogue on a register
+// copy of the env's cold fields (salp::ColdRegs: one round of 16-B loads from
+// its cold block, one of stores), as the rollout's boundary does, instead of
+// one scattered 8-B access per field use.  SALP_LOCKSTEP_COLDREGS=0 keeps the
+// direct accesses (A/B builds).
+#ifndef SALP_LOCKSTEP_COLDREGS
+#define SALP_LOCKSTEP_COLDREGS 1
+#endif
+
 // SalpRobotEnv.step for every env (one breathing cycle each).
 template <bool REC, bool RAND>
 __global__ __launch_bounds__(kBlock) void k_step(double* S, Params P, const float* actions,
                                                  float* obs_out, double* reward_out,
                                                  uint8_t* term_out, uint8_t* trunc_out,
                                                  int auto_reset, float* term_obs_out,
-                                                 double* info_out, SalpTraceBuffer T) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P.n) return;
+                                                 double* info_out, SalpTraceBuffer T, const int32_t* order) {
+    const int64_t lane = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lane >= P.n) return;
+    const int64_t i = order ? (int64_t)order[lane] : lane;   // launch order (salp_sort.hip)
     LANE_CACHE32();
     Hot h;
     salp::load_hot<RAND>(h, S, P, i);
-    salp::begin_step<RAND>(h, S, P, i, actions[3 * i], actions[3 * i + 1], actions[3 * i + 2], c32);
+    float o[SALP_OBS_DIM_MAX];
+    salp::StepOut r;
+    double* info = info_out ? info_out + (size_t)SALP_INFO_DIM * i : nullptr;
+    if (SALP_LOCKSTEP_COLDREGS) {
+        salp::ColdRegs<RAND> C;
+        salp::load_cold<RAND>(C, S, P, i);
+        salp::begin_step<RAND>(h, &C, P, i, actions[3 * i], actions[3 * i + 1], actions[3 * i + 2], c32);
+        salp::store_cold<RAND>(C, S, P, i);
+    } else {
+        salp::begin_step<RAND>(h, S, P, i, actions[3 * i], actions[3 * i + 1], actions[3 * i + 2], c32);
+    }
     if (REC) run_cycle_recorded<RAND>(h, S, P, c32, T, i);
     else run_cycle<RAND>(h, P, c32);
-    SF(SALP_F_STEP_COUNT) = SF(SALP_F_STEP_COUNT) + 1.0;
-    float o[SALP_OBS_DIM_MAX];
-    salp::StepOut r =
-        salp::finish_step<RAND>(h, S, P, i, o, info_out ? info_out + (size_t)SALP_INFO_DIM * i : nullptr);
+    if (SALP_LOCKSTEP_COLDREGS) {
+        salp::ColdRegs<RAND> C;
+        salp::load_cold<RAND>(C, S, P, i);
+        double& sc = salp::sref(&C, P, i, SALP_F_STEP_COUNT);
+        sc = sc + 1.0;
+        r = salp::finish_step<RAND>(h, &C, P, i, o, info);
+        if (term_obs_out)
+            for (int k = 0; k < P.obs_dim; ++k) term_obs_out[(size_t)i * P.obs_dim + k] = o[k];
+        if (auto_reset && (r.terminated || r.truncated)) salp::reset_env_philox(h, &C, P, i, o);
+        salp::store_cold<RAND>(C, S, P, i);
+    } else {
+        SF(SALP_F_STEP_COUNT) = SF(SALP_F_STEP_COUNT) + 1.0;
+        r = salp::finish_step<RAND>(h, S, P, i, o, info);
+        if (term_obs_out)
+            for (int k = 0; k < P.obs_dim; ++k) term_obs_out[(size_t)i * P.obs_dim + k] = o[k];
+        if (auto_reset && (r.terminated || r.truncated)) salp::reset_env_philox(h, S, P, i, o);
+    }
     if (reward_out) reward_out[i] = r.reward;
     if (term_out) term_out[i] = r.terminated;
     if (trunc_out) trunc_out[i] = r.truncated;
-    if (term_obs_out)
-        for (int k = 0; k < P.obs_dim; ++k) term_obs_out[(size_t)i * P.obs_dim + k] = o[k];
-    if (auto_reset && (r.terminated || r.truncated)) salp::reset_env_philox(h, S, P, i, o);
     if (obs_out)
         for (int k = 0; k < P.obs_dim; ++k) obs_out[(size_t)i * P.obs_dim + k] = o[k];
     salp::store_hot<RAND>(h, S, P, i);
@@ -127,27 +157,78 @@ __global__ __launch_bounds__(kBlock) void k_step(double* S, Params P, const floa
 // Lock-step random-action env steps (every env does exactly n_steps).
 template <bool RAND>
 __global__ __launch_bounds__(kBlock) void k_step_random(double* S, Params P, int32_t n_steps,
-                                                        double* reward_sum) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P.n) return;
+                                                        double* reward_sum, const int32_t* order) {
+    const int64_t lane = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lane >= P.n) return;
+    const int64_t i = order ? (int64_t)order[lane] : lane;   // launch order (salp_sort.hip)
     LANE_CACHE32();
     Hot h;
     salp::load_hot<RAND>(h, S, P, i);
     const uint64_t env_id = (uint64_t)(P.env_offset + i);
     double rs = 0.0;
-    for (int32_t k = 0; k < n_steps; ++k) {
-        float a[3];
-        sp_action(P.seed, env_id, (uint64_t)SF(SALP_F_STEP_COUNT), a);
-        salp::begin_step<RAND>(h, S, P, i, a[0], a[1], a[2], c32);
-        run_cycle<RAND>(h, P, c32);
-        SF(SALP_F_STEP_COUNT) = SF(SALP_F_STEP_COUNT) + 1.0;
-        float o[SALP_OBS_DIM_MAX];
-        salp::StepOut r = salp::finish_step<RAND>(h, S, P, i, o, nullptr);
-        rs += r.reward;
-        if (r.terminated || r.truncated) salp::reset_env_philox(h, S, P, i, o);
+    if (SALP_LOCKSTEP_COLDREGS) {
+        // prologue of step k and epilogue of step k - 1 share one cold round
+        salp::ColdRegs<RAND> C;
+        if (n_steps > 0) {
+            salp::load_cold<RAND>(C, S, P, i);
+            float a[3];
+            sp_action(P.seed, env_id, (uint64_t)salp::sref(&C, P, i, SALP_F_STEP_COUNT), a);
+            salp::begin_step<RAND>(h, &C, P, i, a[0], a[1], a[2], c32);
+            salp::store_cold<RAND>(C, S, P, i);
+        }
+        for (int32_t k = 0; k < n_steps; ++k) {
+            run_cycle<RAND>(h, P, c32);
+            salp::load_cold<RAND>(C, S, P, i);
+            double& sc = salp::sref(&C, P, i, SALP_F_STEP_COUNT);
+            sc = sc + 1.0;
+            float o[SALP_OBS_DIM_MAX];
+            salp::StepOut r = salp::finish_step<RAND>(h, &C, P, i, o, nullptr);
+            rs += r.reward;
+            if (r.terminated || r.truncated) salp::reset_env_philox(h, &C, P, i, o);
+            if (k + 1 < n_steps) {
+                float a[3];
+                sp_action(P.seed, env_id, (uint64_t)sc, a);
+                salp::begin_step<RAND>(h, &C, P, i, a[0], a[1], a[2], c32);
+            }
+            salp::store_cold<RAND>(C, S, P, i);
+        }
+    } else {
+        for (int32_t k = 0; k < n_steps; ++k) {
+            float a[3];
+            sp_action(P.seed, env_id, (uint64_t)SF(SALP_F_STEP_COUNT), a);
+            salp::begin_step<RAND>(h, S, P, i, a[0], a[1], a[2], c32);
+            run_cycle<RAND>(h, P, c32);
+            SF(SALP_F_STEP_COUNT) = SF(SALP_F_STEP_COUNT) + 1.0;
+            float o[SALP_OBS_DIM_MAX];
+            salp::StepOut r = salp::finish_step<RAND>(h, S, P, i, o, nullptr);
+            rs += r.reward;
+            if (r.terminated || r.truncated) salp::reset_env_philox(h, S, P, i, o);
+        }
     }
     if (reward_sum) reward_sum[i] = rs;
     salp::store_hot<RAND>(h, S, P, i);
+}
+
+// Sort keys of the lock-step launch order: the predicted ticks of the env's
+// next env-step (the given actions) or next n_steps random env-steps.
+__global__ __launch_bounds__(kBlock) void k_predict_ticks(const double* S, Params P, const float* actions,
+                                                          int32_t n_steps, uint32_t* keys, int32_t* ids) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    double a1 = SF(SALP_F_ANGLE1), a2 = SF(SALP_F_ANGLE2);
+    int64_t t = 0;
+    if (actions) {
+        t = salp::predict_cycle_ticks(P, actions[3 * i], actions[3 * i + 1], actions[3 * i + 2], &a1, &a2);
+    } else {
+        const uint64_t env_id = (uint64_t)(P.env_offset + i), sc = (uint64_t)SF(SALP_F_STEP_COUNT);
+        for (int32_t k = 0; k < n_steps; ++k) {
+            float a[3];
+            sp_action(P.seed, env_id, sc + (uint64_t)k, a);
+            t += salp::predict_cycle_ticks(P, a[0], a[1], a[2], &a1, &a2);
+        }
+    }
+    keys[i] = (uint32_t)(t > 65535 ? 65535 : t);
+    ids[i] = (int32_t)i;
 }
 
 // Chained random-action rollout, filling the rollout buffer.  Work proceeds in
@@ -164,12 +245,15 @@ __device__ __forceinline__ void rollout_boundary(Hot& h, ST S, const Params& P, 
                                                  uint64_t env_id, bool& pending, bool& active,
                                                  int64_t& steps, int64_t max_steps,
                                                  const SalpRolloutBuffers& B, salp::Cache32 c32) {
+    // o: the env's current observation once this boundary has produced one
+    // (after a finished step, or the reset obs after an episode end)
+    float o[SALP_OBS_DIM_MAX];
+    bool have_o = false;
     // a few rounds so that zero-tick cycles chain without waiting a chunk
     for (int rep = 0; rep < 4; ++rep) {
         const bool fin = active && pending && !(h.ct < h.b2);
         if (fin) {
             SF(SALP_F_STEP_COUNT) = SF(SALP_F_STEP_COUNT) + 1.0;
-            float o[SALP_OBS_DIM_MAX];
             salp::StepOut r = salp::finish_step<RAND>(h, S, P, i, o, nullptr);
             if (B.capacity > 0) {
                 const size_t slot = (size_t)(steps % B.capacity);
@@ -186,11 +270,23 @@ __device__ __forceinline__ void rollout_boundary(Hot& h, ST S, const Params& P, 
             }
             ++steps;
             pending = false;
-            if (r.terminated || r.truncated) salp::reset_env_philox(h, S, P, i, nullptr);
+            if (r.terminated || r.truncated) salp::reset_env_philox(h, S, P, i, B.obs_before ? o : nullptr);
+            have_o = true;
             if (max_steps > 0 && steps >= max_steps) active = false;
         }
         const bool beg = active && !pending;
         if (beg) {
+            if (B.obs_before && B.capacity > 0) {
+                // the observation this step's action is taken on: the one just
+                // produced, else (first step after create / reset / set_state)
+                // the env's observation as reset() returns it (noise-free)
+                if (!have_o) {
+                    const salp::Rot R = salp::rot_zyx(h.e0, h.e1, h.e2);
+                    salp::observation(h, R, S, P, i, o);
+                }
+                const size_t row = (size_t)(steps % B.capacity) * (size_t)P.n + (size_t)i;
+                for (int k = 0; k < P.obs_dim; ++k) B.obs_before[row * P.obs_dim + k] = o[k];
+            }
             float a[3];
             sp_action(P.seed, env_id, (uint64_t)SF(SALP_F_STEP_COUNT), a);
             salp::begin_step<RAND>(h, S, P, i, a[0], a[1], a[2], c32);
@@ -255,10 +351,11 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
             if (need) {
                 const RolloutArgs a = fresh_args();
                 const uint64_t env_id = (uint64_t)(a.P.env_offset + i);
-                Hot hb;
-                salp::unspill<RAND>(hb, sp, a.P, env_id);
+                // cold loads first: their HBM latency hides under the LDS unspill
                 salp::ColdRegs<RAND> C;
                 salp::load_cold<RAND>(C, a.S, a.P, i);
+                Hot hb;
+                salp::unspill<RAND>(hb, sp, a.P, env_id);
                 rollout_boundary<RAND>(hb, &C, a.P, i, env_id, pending, active, steps, a.max_steps, a.B, c32);
                 salp::store_cold<RAND>(C, a.S, a.P, i);
                 salp::spill<RAND>(hb, sp);
@@ -278,6 +375,20 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
             if (h.ct < h.b2) salp::tick<false, RAND, true>(h, PV, c32);
     }
     if (A.B.steps_done) A.B.steps_done[i] = steps;
+}
+
+// The ABI's field-major state (state[f * n + i]) <-> the handle's layout
+// (field-major rows + env-major cold block, salp_device.h "state layout").
+// One env per lane; the field-major side is coalesced per field.
+template <bool TO_HANDLE>
+__global__ __launch_bounds__(kBlock) void k_state_copy(double* S, Params P, double* flat) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    for (int f = 0; f < SALP_NUM_FIELDS; ++f) {
+        const size_t a = (size_t)f * (size_t)P.n + (size_t)i;
+        if (TO_HANDLE) SF(f) = flat[a];
+        else flat[a] = SF(f);
+    }
 }
 
 // ------------------------------------------------ Robot / Nozzle level
@@ -403,6 +514,13 @@ struct SalpEnv {
     double* state = nullptr;
     SalpTraceBuffer trace{};   // max_samples 0: not recording
     std::string err;
+    // lock-step launch order (salp_sort.hip): -1 auto, 0 env order, 1 sorted
+    int order_mode = -1;
+    int64_t resident_lanes = 0;   // lanes of one wave per SIMD on this device
+    uint32_t *sort_keys = nullptr, *sort_keys_out = nullptr;
+    int32_t *sort_ids = nullptr, *sort_order = nullptr;
+    void* sort_temp = nullptr;
+    size_t sort_temp_bytes = 0;
 };
 
 namespace {
@@ -462,6 +580,7 @@ Params derive(const SalpParams& p, int64_t n, uint64_t seed, int64_t offset) {
     d.rand_obs = p.observation_randomization != 0;
     d.latency = p.latency != 0;
     d.n = n;
+    d.cold_off = salp::layout_cold_off(n);
     d.env_offset = offset;
     d.seed = seed;
     return d;
@@ -474,6 +593,11 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t salp_ppo_loss_launch
     const float* old_logp, const float* adv, const float* returns, double clip_range, double ent_coef,
     double vf_coef, int normalize_advantage, double* workspace, float* out, float* dmu, float* dvalue,
     void* stream);
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t salp_sort_temp_bytes(int64_t n, size_t* bytes);
+extern "C" __attribute__((visibility("hidden"))) hipError_t salp_sort_launch(
+    void* temp, size_t temp_bytes, const uint32_t* keys_in, uint32_t* keys_out, const int32_t* ids_in,
+    int32_t* order, int64_t n, void* stream);
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t salp_gae_launch(
     int64_t n_steps, int64_t n_envs, const float* rewards, const float* values, const float* episode_starts,
@@ -510,9 +634,23 @@ int salp_create(const SalpParams* p, int64_t n_envs, uint64_t seed, int64_t env_
     h->dp = derive(*p, n_envs, seed, env_id_offset);
     int rc = check_hip(nullptr, hipSetDevice(device), "hipSetDevice");
     if (rc) { delete h; return rc; }
-    rc = check_hip(nullptr, hipMalloc(&h->state, sizeof(double) * SALP_NUM_FIELDS * (size_t)n_envs),
+    rc = check_hip(nullptr, hipMalloc(&h->state, sizeof(double) * (size_t)salp::layout_doubles(n_envs)),
                    "hipMalloc(state)");
     if (rc) { delete h; return SALP_ENOMEM; }
+    {   // lock-step ordering buffers (small: 16 B per env + the sort's scratch)
+        int cus = 0;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+        h->resident_lanes = (int64_t)cus * 4 * 64;   // the lock-step kernels run one wave per SIMD
+        size_t tb = 0;
+        rc = check_hip(nullptr, salp_sort_temp_bytes(n_envs, &tb), "salp_sort_temp_bytes");
+        if (!rc) rc = check_hip(nullptr, hipMalloc(&h->sort_keys, sizeof(uint32_t) * n_envs), "hipMalloc(sort)");
+        if (!rc) rc = check_hip(nullptr, hipMalloc(&h->sort_keys_out, sizeof(uint32_t) * n_envs), "hipMalloc(sort)");
+        if (!rc) rc = check_hip(nullptr, hipMalloc(&h->sort_ids, sizeof(int32_t) * n_envs), "hipMalloc(sort)");
+        if (!rc) rc = check_hip(nullptr, hipMalloc(&h->sort_order, sizeof(int32_t) * n_envs), "hipMalloc(sort)");
+        if (!rc) rc = check_hip(nullptr, hipMalloc(&h->sort_temp, tb > 0 ? tb : 1), "hipMalloc(sort)");
+        h->sort_temp_bytes = tb;
+        if (rc) { g_last_error = h->err.empty() ? g_last_error : h->err; salp_destroy(h); return SALP_ENOMEM; }
+    }
     hipLaunchKernelGGL(k_construct, dim3(blocks_for(n_envs)), dim3(kBlock), 0, nullptr, h->state, h->dp);
     if ((rc = launched(h, "k_construct"))) { g_last_error = h->err; salp_destroy(h); return rc; }
     // SalpRobotEnv.__init__ ends with self.reset() (src/salp_robot_env.py:112)
@@ -528,10 +666,10 @@ int salp_create(const SalpParams* p, int64_t n_envs, uint64_t seed, int64_t env_
 
 int salp_destroy(SalpEnv* h) {
     if (!h) return SALP_OK;
-    if (h->state) {
-        (void)hipSetDevice(h->device);
-        (void)hipFree(h->state);
-    }
+    (void)hipSetDevice(h->device);
+    for (void* p : {(void*)h->state, (void*)h->sort_keys, (void*)h->sort_keys_out, (void*)h->sort_ids,
+                    (void*)h->sort_order, h->sort_temp})
+        if (p) (void)hipFree(p);
     delete h;
     return SALP_OK;
 }
@@ -565,6 +703,21 @@ int salp_reset_to(SalpEnv* h, const uint8_t* mask, const float* targets, const f
     return launched(h, "k_reset_to");
 }
 
+// The launch order of a lock-step call: nullptr (env order) or the sorted
+// permutation, computed on `stream` ahead of the step kernel.
+static const int32_t* lockstep_order(SalpEnv* h, const float* actions, int32_t n_steps, void* stream, int* rc) {
+    *rc = SALP_OK;
+    const bool sort = h->order_mode == 1 || (h->order_mode == -1 && h->n > h->resident_lanes);
+    if (!sort) return nullptr;
+    hipLaunchKernelGGL(k_predict_ticks, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream, h->state,
+                       h->dp, actions, n_steps, h->sort_keys, h->sort_ids);
+    if ((*rc = launched(h, "k_predict_ticks"))) return nullptr;
+    *rc = check_hip(h, salp_sort_launch(h->sort_temp, h->sort_temp_bytes, h->sort_keys, h->sort_keys_out,
+                                        h->sort_ids, h->sort_order, h->n, stream),
+                    "lock-step order sort");
+    return *rc ? nullptr : h->sort_order;
+}
+
 int salp_step(SalpEnv* h, const float* actions, float* obs_out, double* reward_out,
               uint8_t* terminated_out, uint8_t* truncated_out, int auto_reset,
               float* terminal_obs_out, double* info_out, void* stream) {
@@ -572,17 +725,23 @@ int salp_step(SalpEnv* h, const float* actions, float* obs_out, double* reward_o
     if (!actions) return fail(h, SALP_EINVAL, "salp_step: actions is required");
     auto kern = h->trace.max_samples > 0 ? (randomized(h->dp) ? k_step<true, true> : k_step<true, false>)
                                          : (randomized(h->dp) ? k_step<false, true> : k_step<false, false>);
+    int rc;
+    const int32_t* order = lockstep_order(h, actions, 1, stream, &rc);
+    if (rc) return rc;
     hipLaunchKernelGGL(kern, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream, h->state, h->dp,
                        actions, obs_out, reward_out, terminated_out, truncated_out, auto_reset, terminal_obs_out,
-                       info_out, h->trace);
+                       info_out, h->trace, order);
     return launched(h, "k_step");
 }
 
 int salp_step_random(SalpEnv* h, int32_t n_steps, double* reward_sum_out, void* stream) {
     if (!h) return fail(nullptr, SALP_EINVAL, "salp_step_random: null handle");
     if (n_steps < 0) return fail(h, SALP_EINVAL, "salp_step_random: n_steps < 0");
+    int rc;
+    const int32_t* order = lockstep_order(h, nullptr, n_steps, stream, &rc);
+    if (rc) return rc;
     hipLaunchKernelGGL(randomized(h->dp) ? k_step_random<true> : k_step_random<false>, dim3(blocks_for(h->n)),
-                       dim3(kBlock), 0, (hipStream_t)stream, h->state, h->dp, n_steps, reward_sum_out);
+                       dim3(kBlock), 0, (hipStream_t)stream, h->state, h->dp, n_steps, reward_sum_out, order);
     return launched(h, "k_step_random");
 }
 
@@ -642,6 +801,13 @@ int salp_robot_step_through_cycle(SalpEnv* h, void* stream) {
     return launched(h, "k_robot_cycle");
 }
 
+int salp_set_lockstep_order(SalpEnv* h, int mode) {
+    if (!h) return fail(nullptr, SALP_EINVAL, "salp_set_lockstep_order: null handle");
+    if (mode < -1 || mode > 1) return fail(h, SALP_EINVAL, "salp_set_lockstep_order: mode must be -1, 0 or 1");
+    h->order_mode = mode;
+    return SALP_OK;
+}
+
 int salp_set_trace(SalpEnv* h, const SalpTraceBuffer* buf) {
     if (!h) return fail(nullptr, SALP_EINVAL, "salp_set_trace: null handle");
     if (!buf || buf->max_samples <= 0) {
@@ -677,16 +843,16 @@ int salp_set_randomization(SalpEnv* h, int dynamics, int disturbances, int actio
 
 int salp_get_state(SalpEnv* h, double* state_out, void* stream) {
     if (!h || !state_out) return fail(h, SALP_EINVAL, "salp_get_state: null argument");
-    return check_hip(h, hipMemcpyAsync(state_out, h->state, sizeof(double) * SALP_NUM_FIELDS * (size_t)h->n,
-                                       hipMemcpyDeviceToDevice, (hipStream_t)stream),
-                     "salp_get_state");
+    hipLaunchKernelGGL(k_state_copy<false>, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream, h->state,
+                       h->dp, state_out);
+    return launched(h, "salp_get_state");
 }
 
 int salp_set_state(SalpEnv* h, const double* state_in, void* stream) {
     if (!h || !state_in) return fail(h, SALP_EINVAL, "salp_set_state: null argument");
-    return check_hip(h, hipMemcpyAsync(h->state, state_in, sizeof(double) * SALP_NUM_FIELDS * (size_t)h->n,
-                                       hipMemcpyDeviceToDevice, (hipStream_t)stream),
-                     "salp_set_state");
+    hipLaunchKernelGGL(k_state_copy<true>, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream, h->state,
+                       h->dp, const_cast<double*>(state_in));
+    return launched(h, "salp_set_state");
 }
 
 int salp_math_selftest(const double* x, const double* y, int64_t n, double* out, void* stream) {

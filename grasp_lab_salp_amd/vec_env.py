@@ -35,7 +35,7 @@ import time
 import numpy as np
 import torch
 
-from ._abi import EPISODE_METRIC_KEYS, INFO, REWARD_COMPONENT_KEYS, SalpParams, default_params
+from ._abi import EPISODE_METRIC_KEYS, FIELD, INFO, MAX_OBSTACLES, REWARD_COMPONENT_KEYS, SalpParams, default_params
 from .batched_env import BatchedSalpEnv
 from .spaces import Box
 
@@ -141,38 +141,177 @@ class SalpVecEnv(_VecEnvBase):
                                   env_id_offset=self.sim.env_id_offset, device=self.sim.device.index)
         return [int(seed) + i for i in range(self.num_envs)]
 
+    # ------------------------------------------- per-env attribute access
+    # SB3's VecEnv forwards get_attr / set_attr / env_method to each wrapped
+    # env (EvalCallback and user callbacks rely on per-env answers).  Here
+    # every env is a column of the device state: per-env attributes are read
+    # from / written to that column; attributes of the shared configuration
+    # are the same for every env.
+    _SHARED_ATTRS = ("observation_space", "action_space", "render_mode", "metadata", "num_obstacles", "width",
+                     "height", "obstacle_radius", "params")
+
+    def _indices(self, indices):
+        if indices is None:
+            return list(range(self.num_envs))
+        if isinstance(indices, int):
+            indices = [indices]
+        idx = [int(i) for i in indices]
+        if any(i < 0 or i >= self.num_envs for i in idx):
+            raise IndexError(f"env index out of range [0, {self.num_envs})")
+        return idx
+
+    def _env_attr_values(self, attr_name, idx):
+        """Per-env values of a reference attribute, or None if it is not one."""
+        st = None
+
+        def col(name):
+            nonlocal st
+            if st is None:
+                st = self.sim.get_state().cpu().numpy()
+            return st[FIELD[name]]
+        if attr_name in FIELD:                      # robot / env state by its reference name
+            v = col(attr_name)
+            return [float(v[i]) for i in idx]
+        if attr_name == "target_point":            # src/salp_robot_env.py:114-155
+            t0, t1 = col("target0"), col("target1")
+            return [np.array([t0[i], t1[i]], dtype=np.float32) for i in idx]
+        if attr_name == "obstacles":
+            k = col("n_obst")
+            xy = [col(f"obst{j}") for j in range(2 * MAX_OBSTACLES)]
+            return [[np.array([xy[2 * j][i], xy[2 * j + 1][i]], dtype=np.float32) for j in range(int(k[i]))]
+                    for i in idx]
+        if attr_name in ("episode_length", "episode_reward"):
+            v = col("ep_len" if attr_name == "episode_length" else "ep_return")
+            return [float(v[i]) for i in idx]
+        return None
+
     def get_attr(self, attr_name, indices=None):
-        idx = range(self.num_envs) if indices is None else indices
-        v = getattr(self, attr_name)
-        return [v for _ in idx]
+        """Per env: state attributes (any ``salp_field_name``, ``target_point``,
+        ``obstacles``, ``episode_length``, ``episode_reward``) come from that
+        env's column; configuration attributes are shared."""
+        idx = self._indices(indices)
+        vals = self._env_attr_values(attr_name, idx)
+        if vals is not None:
+            return vals
+        if attr_name in self._SHARED_ATTRS:
+            v = getattr(self, attr_name) if hasattr(self, attr_name) else getattr(self.sim, attr_name)
+            return [v for _ in idx]
+        raise AttributeError(f"SalpRobotEnv has no attribute {attr_name!r}")
 
     def set_attr(self, attr_name, value, indices=None):
-        setattr(self, attr_name, value)
+        """Per env for state attributes (written into those envs' columns);
+        configuration attributes only for all envs at once (one kernel)."""
+        idx = self._indices(indices)
+        if attr_name in FIELD or attr_name == "target_point":
+            st = self.sim.get_state()
+            ii = torch.as_tensor(idx, device=st.device)
+            if attr_name == "target_point":
+                v = torch.as_tensor(np.asarray(value, np.float32), dtype=torch.float64, device=st.device)
+                v = v.reshape(-1, 2).expand(len(idx), 2)
+                st[FIELD["target0"], ii] = v[:, 0]
+                st[FIELD["target1"], ii] = v[:, 1]
+            else:
+                st[FIELD[attr_name], ii] = torch.as_tensor(value, dtype=torch.float64, device=st.device)
+            self.sim.set_state(st)
+            return
+        if attr_name in self._SHARED_ATTRS:
+            if len(idx) != self.num_envs:
+                raise ValueError(f"{attr_name!r} is shared by all envs of the batch; set it for all indices")
+            setattr(self, attr_name, value)
+            return
+        raise AttributeError(f"SalpRobotEnv has no settable attribute {attr_name!r}")
+
+    _BATCH_SWITCHES = {"enable_action_randomization": "actions",
+                       "enable_observation_randomization": "observations", "enable_latency": "latency"}
 
     def env_method(self, method_name, *args, indices=None, **kwargs):
-        idx = range(self.num_envs) if indices is None else indices
-        return [getattr(self, method_name)(*args, **kwargs) for _ in idx]
+        """Per-env reference methods: ``reset`` (the listed envs only; returns
+        their (obs, info)), ``get_cycle_count``, ``sample_random_action``; the
+        randomisation switches ``enable_*`` act on the whole batch, so they need
+        every index.  ``render`` is out of scope."""
+        idx = self._indices(indices)
+        if method_name == "reset":
+            mask = torch.zeros(self.num_envs, dtype=torch.uint8)
+            mask[idx] = 1
+            obs = self.sim.reset(mask=mask).cpu().numpy()
+            return [(obs[i], {}) for i in idx]
+        if method_name == "get_cycle_count":
+            return [int(c) for c in self._env_attr_values("cycle", idx)]
+        if method_name == "sample_random_action":
+            return [self.action_space.sample() for _ in idx]
+        if method_name in self._BATCH_SWITCHES:
+            if len(idx) != self.num_envs:
+                raise ValueError(f"{method_name} switches the whole batch; call it for all indices")
+            p = self.sim.params
+            cur = dict(dynamics=bool(p.dynamics_randomization), disturbances=bool(p.disturbances),
+                       actions=bool(p.action_randomization), observations=bool(p.observation_randomization),
+                       latency=bool(p.latency))
+            cur[self._BATCH_SWITCHES[method_name]] = True
+            self.sim.set_randomization(**cur)
+            return [None for _ in idx]
+        if method_name == "render":
+            raise NotImplementedError("rendering is out of scope")
+        raise AttributeError(f"SalpRobotEnv has no method {method_name!r}")
 
     def env_is_wrapped(self, wrapper_class, indices=None):
-        idx = range(self.num_envs) if indices is None else indices
-        return [False for _ in idx]
+        """Every env behaves as if wrapped in SB3's ``Monitor`` (info["episode"]
+        on the last step of an episode); nothing else wraps it."""
+        idx = self._indices(indices)
+        name = getattr(wrapper_class, "__name__", str(wrapper_class))
+        return [name == "Monitor" for _ in idx]
 
     def get_images(self):
         raise NotImplementedError("rendering is out of scope")
 
 
-def make_vec_env(env_id, n_envs=1, seed=None, vec_env_cls=None, **kwargs):
-    """Stand-in for SB3's ``make_vec_env`` with the reference's ``make_env``:
-    calls ``env_id()`` once to read the robot / env configuration it builds,
-    then returns one :class:`SalpVecEnv` of ``n_envs`` envs (``vec_env_cls`` is
-    accepted and ignored: all envs share one kernel launch)."""
+# SB3's in-process / subprocess VecEnv classes: for the batched simulator both
+# mean "all envs in one kernel launch", which is what SalpVecEnv is.
+_BATCHED_EQUIVALENT = ("DummyVecEnv", "SubprocVecEnv")
+
+
+def make_vec_env(env_id, n_envs=1, seed=None, start_index=0, monitor_dir=None, wrapper_class=None,
+                 env_kwargs=None, vec_env_cls=None, vec_env_kwargs=None, monitor_kwargs=None,
+                 wrapper_kwargs=None):
+    """SB3's ``make_vec_env`` for the reference's ``make_env`` callable
+    (src/train_robot.py:26, src/train_robot_recurrent_ppo.py:65).
+
+    ``make_env`` is called once to read the robot / env configuration it builds.
+    With ``vec_env_cls`` None, SB3's ``DummyVecEnv`` or ``SubprocVecEnv`` (the
+    reference's choices) or a ``SalpVecEnv`` subclass, the result is ONE batched
+    :class:`SalpVecEnv` of ``n_envs`` envs (Monitor semantics built in).  Any
+    other ``vec_env_cls`` is honoured the SB3 way: ``vec_env_cls([make_env] *
+    n_envs, **vec_env_kwargs)`` over the drop-in single envs.  ``wrapper_class``
+    (a gym wrapper per env) also takes that per-env path with DummyVecEnv
+    semantics.  ``monitor_dir`` is not supported (no CSV monitor files)."""
     if not callable(env_id):
         raise TypeError("env_id must be the reference-style make_env callable")
-    env = env_id()
-    try:
-        params = env.robot.salp_params(width=int(env.width), height=int(env.height),
-                                       num_obstacles=int(env.num_obstacles),
-                                       obstacle_radius=float(env.obstacle_radius))
-    finally:
-        env.close()
-    return SalpVecEnv(n_envs, params=params, seed=0 if seed is None else seed)
+    if monitor_dir is not None:
+        raise NotImplementedError("monitor_dir: Monitor CSV files are not written (info['episode'] is)")
+    env_kwargs = env_kwargs or {}
+    cls_name = getattr(vec_env_cls, "__name__", None)
+    batched = (vec_env_cls is None or cls_name in _BATCHED_EQUIVALENT
+               or (isinstance(vec_env_cls, type) and issubclass(vec_env_cls, SalpVecEnv)))
+    if batched and wrapper_class is None:
+        env = env_id(**env_kwargs)
+        try:
+            params = env.robot.salp_params(width=int(env.width), height=int(env.height),
+                                           num_obstacles=int(env.num_obstacles),
+                                           obstacle_radius=float(env.obstacle_radius))
+        finally:
+            env.close()
+        cls = vec_env_cls if (isinstance(vec_env_cls, type) and issubclass(vec_env_cls, SalpVecEnv)) else SalpVecEnv
+        return cls(n_envs, params=params, seed=0 if seed is None else seed, env_id_offset=start_index,
+                   **(vec_env_kwargs or {}) if cls is not SalpVecEnv else {})
+
+    def make(rank):
+        def _init():
+            e = env_id(**env_kwargs)
+            if wrapper_class is not None:
+                e = wrapper_class(e, **(wrapper_kwargs or {}))
+            return e
+        return _init
+    fns = [make(i + start_index) for i in range(n_envs)]
+    if vec_env_cls is None or cls_name in _BATCHED_EQUIVALENT:
+        if cls_name is None:
+            raise ValueError("wrapper_class needs a per-env vec_env_cls (e.g. SB3's DummyVecEnv)")
+    return vec_env_cls(fns, **(vec_env_kwargs or {}))

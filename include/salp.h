@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define SALP_ABI_VERSION 3
+#define SALP_ABI_VERSION 4
 
 #define SALP_MAX_OBSTACLES 4
 #define SALP_OBS_DIM_MAX (6 + 2 * SALP_MAX_OBSTACLES)
@@ -103,6 +103,10 @@ typedef struct SalpRolloutBuffers {
                             * reaches it (fixed-length rollouts, n_steps)     */
     int32_t chunk;         /* ticks between env-step boundaries (0 = 128)     */
     int32_t reserved;
+    float* obs_before;     /* [capacity][n_envs][obs_dim]  the observation the
+                            * step's action was taken from (SB3 RolloutBuffer
+                            * "obs"): the previous step's obs, or the reset obs
+                            * after an episode end (ABI 4)                     */
 } SalpRolloutBuffers;
 
 /* ------------------------------------------------------------ lifecycle */
@@ -144,6 +148,14 @@ int salp_rollout(SalpEnv* h, int64_t tick_budget, const SalpRolloutBuffers* buf,
 /* Same random actions, lock-step: every env performs exactly n_steps
  * env-steps (one full cycle each) with auto-reset.  rewards_out [n] = sum. */
 int salp_step_random(SalpEnv* h, int32_t n_steps, double* reward_sum_out, void* stream);
+
+/* Launch order of the lock-step calls (salp_step, salp_step_random): a
+ * launch lasts as long as its slowest wave.  mode 1: envs run sorted by the
+ * predicted length of the cycle each is about to run (longest first), which
+ * packs the waves once there are more envs than one wave per SIMD can hold;
+ * 0: env order; -1 (default): sorted exactly when n_envs exceeds that.
+ * Results per env are identical in every mode. */
+int salp_set_lockstep_order(SalpEnv* h, int mode);
 
 /* GAE / returns over a rollout buffer: stable_baselines3's
  * RolloutBuffer.compute_returns_and_advantage (stable-baselines3 >= 2.0,
@@ -239,7 +251,10 @@ int salp_set_state(SalpEnv* h, const double* state_in, void* stream);
  * (a cycle that ends simply continues in REST); times the tick body alone.
  * Leaves the envs in a state no reference call sequence produces. */
 int salp_bench_ticks(SalpEnv* h, int32_t n_ticks, void* stream);
-/* Device address of the handle's state buffer (zero-copy views). */
+/* Device address of the handle's state buffer.  Its layout is internal
+ * (field-major rows plus an env-major block of the fields only env-step
+ * boundaries touch, grasp_lab_salp_amd/csrc/salp_device.h "state layout");
+ * use salp_get_state / salp_set_state for the field-major view. */
 int64_t salp_state_ptr(SalpEnv* h);
 /* Device-side self-test of salp_math.h: out[i] = f(x[i]) for f in
  * {sin, cos, tan, atan2(x, y), asin, acos, cube, np_cosf, np_sinf, sin and cos

@@ -58,3 +58,29 @@ def test_create_rejects_bad_arguments_without_touching_the_gpu(lib):
     p = _abi.default_params()
     assert lib.salp_create(ctypes.byref(p), 0, 0, 0, 0, ctypes.byref(h)) == -1
     assert lib.salp_step(None, None, None, None, None, None, 0, None, None, None) == -1
+
+
+def _header_struct_fields(name):
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    body = re.search(r"typedef struct " + name + r"\s*\{(.*?)\}\s*" + name + ";", text, flags=re.S).group(1)
+    fields = []
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        first, *rest = decl.split(",")
+        fields.append(re.findall(r"(\w+)\s*$", first.strip())[0])
+        fields += [r.strip().lstrip("*").strip() for r in rest]
+    return fields
+
+
+@pytest.mark.parametrize("name,cls", [("SalpParams", _abi.SalpParams), ("SalpRolloutBuffers", _lib.SalpRolloutBuffers),
+                                      ("SalpTraceBuffer", _lib.SalpTraceBuffer)])
+def test_struct_layouts_match_header(name, cls):
+    """The ctypes mirrors declare the header's fields in the header's order."""
+    assert _header_struct_fields(name) == [f for f, _ in cls._fields_]
+
+
+def test_abi_version(lib):
+    assert lib.salp_abi_version() == _abi.ABI_VERSION
+    assert f"#define SALP_ABI_VERSION {_abi.ABI_VERSION}" in open(HEADER).read()

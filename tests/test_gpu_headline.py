@@ -54,6 +54,7 @@ def _bits_equal(x, y):
 
 def _buffers(cap, n, dev="cuda"):
     return {"obs": torch.full((cap, n, 10), -7.0, device=dev),
+            "obs_before": torch.full((cap, n, 10), -7.0, device=dev),
             "actions": torch.full((cap, n, 3), -7.0, device=dev),
             "rewards": torch.full((cap, n), -7.0, device=dev),
             "dones": torch.full((cap, n), 255, dtype=torch.uint8, device=dev)}
@@ -92,7 +93,7 @@ def _oracle_rollout(seed, start, n, steps, env_offset_base=0):
     """The chained rollout per env == env-steps with Philox actions keyed by
     (seed, global id, step count) and auto-reset: the oracle step by step."""
     o = orc.Oracle(default_params(), n, seed=seed, env_offset=env_offset_base + start)
-    o.reset()
+    obs0 = o.reset()
     outs, acts = [], []
     for _ in range(steps):
         act = np.zeros((n, 3), np.float32)
@@ -101,17 +102,19 @@ def _oracle_rollout(seed, start, n, steps, env_offset_base=0):
             act[i] = philox_action(seed, env_offset_base + start + i, int(sc[i]))
         outs.append(o.step(act, auto_reset=True))
         acts.append(act)
-    return o, acts, outs
+    return o, acts, outs, obs0
 
 
 def _check_blocks(env, bufs, done, steps, blocks, seed, base=0):
     g = _cpu(env.get_state())
     assert int(done.min()) == steps and int(done.max()) == steps
     for start, n in blocks:
-        o, acts, outs = _oracle_rollout(seed, start, n, steps, base)
+        o, acts, outs, obs0 = _oracle_rollout(seed, start, n, steps, base)
         sl = slice(start, start + n)
         assert_state_equal(g[:, sl], o.state, f"block {base + start}")
         for t in range(steps):
+            before = obs0 if t == 0 else outs[t - 1]["obs"]
+            assert np.array_equal(_cpu(bufs["obs_before"][t, sl]), before, equal_nan=True), (start, t)
             assert np.array_equal(_cpu(bufs["actions"][t, sl]), acts[t]), (start, t)
             assert np.array_equal(_cpu(bufs["obs"][t, sl]), outs[t]["terminal_obs"], equal_nan=True), (start, t)
             assert np.array_equal(_cpu(bufs["rewards"][t, sl]), outs[t]["reward"].astype(np.float32),

@@ -177,6 +177,7 @@ def test_rollout_is_split_invariant_and_matches_oracle():
     b = BatchedSalpEnv(n, params=p, seed=21)
     cap = steps
     bufs = {"obs": torch.zeros((cap, n, 10), device="cuda"),
+            "obs_before": torch.zeros((cap, n, 10), device="cuda"),
             "actions": torch.zeros((cap, n, 3), device="cuda"),
             "rewards": torch.zeros((cap, n), device="cuda"),
             "dones": torch.zeros((cap, n), dtype=torch.uint8, device="cuda")}
@@ -192,7 +193,7 @@ def test_rollout_is_split_invariant_and_matches_oracle():
     ga, gb = _cpu(a.get_state()), _cpu(b.get_state())
     assert np.array_equal(ga, gb, equal_nan=True)
     o = orc.Oracle(p, n, seed=21)
-    o.reset()
+    obs0 = o.reset()
     # oracle step-by-step with the same Philox actions
     from grasp_lab_salp_amd._abi import FIELD as FF
     acts = []
@@ -208,6 +209,10 @@ def test_rollout_is_split_invariant_and_matches_oracle():
     for t in range(steps):
         assert np.array_equal(_cpu(bufs["actions"][t]), acts[t])
         assert np.array_equal(_cpu(bufs["obs"][t]), outs[t]["terminal_obs"], equal_nan=True)
+        # the observation the action was taken on: reset obs, then each step's
+        # returned obs (the reset obs where the previous step ended an episode)
+        before = obs0 if t == 0 else outs[t - 1]["obs"]
+        assert np.array_equal(_cpu(bufs["obs_before"][t]), before, equal_nan=True), t
         assert np.array_equal(_cpu(bufs["rewards"][t]), outs[t]["reward"].astype(np.float32), equal_nan=True)
         dn = outs[t]["terminated"] | (outs[t]["truncated"] << 1)
         assert np.array_equal(_cpu(bufs["dones"][t]), dn)
@@ -294,3 +299,34 @@ def test_float32_shape_carried_across_cycles():
         if t == 0:   # (almost all) even lanes end the cycle in the float32 REFILL shape
             in32 = (o.state[FIELD["geom32"], sel] == 1) & (o.state[FIELD["phase"], sel] == 0)
             assert in32.mean() > 0.9
+
+
+@pytest.mark.parametrize("n", [3000, 200_000])
+def test_sorted_lockstep_order_changes_nothing_but_time(n):
+    """salp_set_lockstep_order: the lock-step kernels run envs sorted by their
+    predicted cycle length (auto above one wave per SIMD, i.e. at 200 000
+    envs).  Per-env results are bit-identical to env order, and to the oracle
+    on a block of envs."""
+    p = default_params()
+    a = BatchedSalpEnv(n, params=p, seed=12)
+    b = BatchedSalpEnv(n, params=p, seed=12)
+    a.set_lockstep_order(1)
+    b.set_lockstep_order(0)
+    ra, rb = a.step_random(2), b.step_random(2)
+    rng = np.random.default_rng(4)
+    act = torch.tensor(random_actions(rng, n), device="cuda")
+    sa, sb = a.step(act, auto_reset=True), b.step(act, auto_reset=True)
+    assert torch.equal(ra.view(torch.int64), rb.view(torch.int64))
+    for x, y in ((sa.obs, sb.obs), (sa.reward, sb.reward), (sa.info, sb.info)):
+        assert torch.equal(x.contiguous().view(torch.int32 if x.dtype == torch.float32 else torch.int64),
+                           y.contiguous().view(torch.int32 if y.dtype == torch.float32 else torch.int64))
+    assert torch.equal(sa.terminated, sb.terminated) and torch.equal(sa.truncated, sb.truncated)
+    ga = a.get_state()
+    assert torch.equal(ga.view(torch.int64), b.get_state().view(torch.int64))
+    # and the envs are the reference's: oracle on a block of global ids
+    lo = n // 2
+    o = orc.Oracle(p, 512, seed=12, env_offset=lo)
+    o.reset()
+    o.step_random(2)
+    o.step(_cpu(act)[lo:lo + 512], auto_reset=True)
+    assert_state_equal(_cpu(ga)[:, lo:lo + 512], o.state, "sorted lock-step block")
