@@ -320,7 +320,6 @@ class PPO:
         self.n_envs = self.sim.n_envs
         self.obs_dim = self.sim.obs_dim
         self.act_dim = 3
-        g = torch.Generator(device="cpu").manual_seed(int(seed))
         torch.manual_seed(int(seed))
         self.policy = (policy if isinstance(policy, nn.Module) else ActorCritic(self.obs_dim, self.act_dim)).to(
             self.device)
@@ -353,7 +352,11 @@ class PPO:
         self._nonfinite = torch.zeros((), dtype=torch.int64, device=self.device)
         # finished-episode statistics of the current collection (device, sync-free)
         self._ep_stats = torch.zeros(2, dtype=torch.float64, device=self.device)
-        self.gen = g
+        # minibatch permutations are drawn on the device: SB3 permutes on the
+        # host (np.random.permutation), which at n_steps 2048 x 32 768 envs is
+        # a 537 MB index array per epoch to build and upload
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(int(seed))
         self.buf = RolloutBuffer(self.n_steps, self.n_envs, self.obs_dim, self.act_dim, self.device)
         self.low = torch.tensor([0.0, 0.0, -1.0], device=self.device)
         self.high = torch.tensor([1.0, 1.0, 1.0], device=self.device)
@@ -500,7 +503,7 @@ class PPO:
         acc = torch.zeros(4, device=self.device)
         steps = 0
         for _ in range(self.n_epochs):
-            perm = torch.randperm(N, generator=self.gen).to(self.device)
+            perm = torch.randperm(N, generator=self.gen, device=self.device)
             for s in range(0, N, self.batch_size):
                 idx = perm[s:s + self.batch_size]
                 if self.use_graphs and idx.numel() == self.batch_size:
