@@ -330,3 +330,20 @@ def test_sorted_lockstep_order_changes_nothing_but_time(n):
     o.step_random(2)
     o.step(_cpu(act)[lo:lo + 512], auto_reset=True)
     assert_state_equal(_cpu(ga)[:, lo:lo + 512], o.state, "sorted lock-step block")
+
+
+@pytest.mark.parametrize("n", [1, 255, 4099])
+def test_state_round_trip_through_the_hbm_layout(n):
+    """salp_set_state / salp_get_state convert between the ABI's field-major
+    view and the handle's layout (rows + env-major cold block): any bit
+    pattern, NaNs and signed zeros included, comes back unchanged; ragged
+    sizes exercise the padded cold-block offset."""
+    env = BatchedSalpEnv(n, params=default_params(), seed=1)
+    g = torch.Generator().manual_seed(n)
+    bits = torch.randint(-2**62, 2**62, (NUM_FIELDS, n), generator=g, dtype=torch.int64)
+    st = bits.view(torch.float64).clone()
+    st[0, 0] = float("nan")
+    st[1, 0] = -0.0
+    env.set_state(st)
+    back = env.get_state().cpu()
+    assert torch.equal(back.view(torch.int64), st.view(torch.int64))

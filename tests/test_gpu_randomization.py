@@ -118,3 +118,34 @@ def test_switching_randomization_off_restores_reference_behaviour():
     g = _cpu(env.get_state())
     assert np.all(g[FIELD["cd"]] == 0.3)
     assert_state_equal(g, o.state, "after switching off")
+
+
+def test_randomized_sorted_lockstep_and_rollout_at_scale():
+    """Every switch on, 70 000 envs (more than one wave per SIMD: the lock-step
+    call runs in sorted order, and the RAND kernels carry the randomisation
+    fields in rows beside the env-major cold block): sorted == env order bit
+    for bit, both == the oracle on a block; then a chained rollout on top."""
+    n = 70_000
+    p = default_params()
+    a = BatchedSalpEnv(n, params=p, seed=21)
+    b = BatchedSalpEnv(n, params=p, seed=21)
+    for e in (a, b):
+        e.set_randomization(**ALL)
+    a.set_lockstep_order(1)
+    b.set_lockstep_order(0)
+    ra, rb = a.step_random(2), b.step_random(2)
+    assert torch.equal(ra.view(torch.int64), rb.view(torch.int64))
+    ga = a.get_state()
+    assert torch.equal(ga.view(torch.int64), b.get_state().view(torch.int64))
+    lo = 40_000
+    o = orc.Oracle(p, 256, seed=21, env_offset=lo)
+    o.set_randomization(**ALL)
+    o.reset()
+    rs_o, _ = o.step_random(2)
+    assert np.array_equal(_cpu(ra)[lo:lo + 256], rs_o, equal_nan=True)
+    assert_state_equal(_cpu(ga)[:, lo:lo + 256], o.state, "RAND sorted lock-step")
+    done = torch.zeros(n, dtype=torch.int64, device="cuda")
+    a.rollout(3000, steps_done=done, max_steps=2)
+    o.step_random(2)
+    assert int(done.min()) == 2
+    assert_state_equal(_cpu(a.get_state())[:, lo:lo + 256], o.state, "RAND rollout after lock-step")
