@@ -159,8 +159,8 @@ class BatchedSalpEnv:
     def set_lockstep_order(self, mode):
         """Launch order of :meth:`step` / :meth:`step_random` (salp_set_lockstep_order):
         1 = envs sorted by the predicted length of their next cycle, 0 = env
-        order, -1 = sorted when there are more envs than one wave per SIMD
-        holds (default).  Results are identical in every mode."""
+        order, -1 = sorted from 1 024 envs on (default).  Results are identical
+        in every mode."""
         self._check(_lib.load().salp_set_lockstep_order(self._h, int(mode)))
 
     def rollout(self, tick_budget, buffers=None, steps_done=None, max_steps=0, chunk=128):

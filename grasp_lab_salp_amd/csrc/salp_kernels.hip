@@ -24,6 +24,8 @@ constexpr int kBlock = 256;
 // Longest legitimate cycle: max(refill 3.3 s, turn 3.9 s) + jet 0.5 s + coast
 // 10 s < 1500 ticks.  The guard only bounds a lane fed a corrupted state.
 constexpr int kMaxTicksPerCycle = 1 << 16;
+// Lock-step launches of at least this many envs run in sorted order by default.
+constexpr int64_t kSortMinEnvs = 1024;
 
 static_assert(kBlock == salp::LANES, "LDS cache stride is the workgroup size");
 
@@ -516,7 +518,6 @@ struct SalpEnv {
     std::string err;
     // lock-step launch order (salp_sort.hip): -1 auto, 0 env order, 1 sorted
     int order_mode = -1;
-    int64_t resident_lanes = 0;   // lanes of one wave per SIMD on this device
     uint32_t *sort_keys = nullptr, *sort_keys_out = nullptr;
     int32_t *sort_ids = nullptr, *sort_order = nullptr;
     void* sort_temp = nullptr;
@@ -638,9 +639,6 @@ int salp_create(const SalpParams* p, int64_t n_envs, uint64_t seed, int64_t env_
                    "hipMalloc(state)");
     if (rc) { delete h; return SALP_ENOMEM; }
     {   // lock-step ordering buffers (small: 16 B per env + the sort's scratch)
-        int cus = 0;
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-        h->resident_lanes = (int64_t)cus * 4 * 64;   // the lock-step kernels run one wave per SIMD
         size_t tb = 0;
         rc = check_hip(nullptr, salp_sort_temp_bytes(n_envs, &tb), "salp_sort_temp_bytes");
         if (!rc) rc = check_hip(nullptr, hipMalloc(&h->sort_keys, sizeof(uint32_t) * n_envs), "hipMalloc(sort)");
@@ -707,7 +705,9 @@ int salp_reset_to(SalpEnv* h, const uint8_t* mask, const float* targets, const f
 // permutation, computed on `stream` ahead of the step kernel.
 static const int32_t* lockstep_order(SalpEnv* h, const float* actions, int32_t n_steps, void* stream, int* rc) {
     *rc = SALP_OK;
-    const bool sort = h->order_mode == 1 || (h->order_mode == -1 && h->n > h->resident_lanes);
+    // auto: sorted from a few waves on (measured: +10 % with every wave
+    // resident, 1.8x at two waves per SIMD; profiles/r2_experiments.md r2e)
+    const bool sort = h->order_mode == 1 || (h->order_mode == -1 && h->n >= kSortMinEnvs);
     if (!sort) return nullptr;
     hipLaunchKernelGGL(k_predict_ticks, dim3(blocks_for(h->n)), dim3(kBlock), 0, (hipStream_t)stream, h->state,
                        h->dp, actions, n_steps, h->sort_keys, h->sort_ids);

@@ -18,8 +18,8 @@ scan (HIP kernel ``salp_gae``) and the policy all stay in HBM:
   averaged with one flat all-reduce per minibatch (torch.distributed, ``nccl``
   = RCCL over xGMI; the MLP's gradients are ~20 KB, so one bucket);
 * single GPU: the whole minibatch update (forward, backward, clipping, Adam)
-  is captured once into a HIP graph and replayed per minibatch; the small MLP
-  is otherwise bound by ~60 kernel launches per step.
+  is captured into a HIP graph once per update and replayed per minibatch;
+  the small MLP is otherwise bound by ~60 kernel launches per step.
 
 The policy is SB3's ``MlpPolicy`` for PPO (separate 64-64 tanh actor and critic,
 orthogonal init, state-independent log-std).  The reference's RecurrentPPO
@@ -499,7 +499,15 @@ class PPO:
         self._graph.replay()
 
     def train(self):
+        """n_epochs passes of minibatch updates over the rollout buffer.  The
+        HIP graph of the minibatch step is captured afresh for every update
+        (three warm-up steps, one capture, replays): a graph kept from one
+        update to the next went stale after a collection (from the second or
+        third update on its replays left all-zero, then NaN, gradients while
+        the same minibatch computed eagerly was finite;
+        tools/debug_ppo_drift.py)."""
         N = self.n_steps * self.n_envs
+        self._graph, self._graph_warm = None, 0
         acc = torch.zeros(4, device=self.device)
         steps = 0
         for _ in range(self.n_epochs):

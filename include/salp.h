@@ -151,10 +151,11 @@ int salp_step_random(SalpEnv* h, int32_t n_steps, double* reward_sum_out, void* 
 
 /* Launch order of the lock-step calls (salp_step, salp_step_random): a
  * launch lasts as long as its slowest wave.  mode 1: envs run sorted by the
- * predicted length of the cycle each is about to run (longest first), which
- * packs the waves once there are more envs than one wave per SIMD can hold;
- * 0: env order; -1 (default): sorted exactly when n_envs exceeds that.
- * Results per env are identical in every mode. */
+ * predicted length of the cycle each is about to run (longest first): the
+ * waves of short cycles finish early, which lets the chip clock the long ones
+ * higher, and beyond one wave per SIMD the rounds pack; 0: env order;
+ * -1 (default): sorted from 1 024 envs on.  Results per env are identical in
+ * every mode. */
 int salp_set_lockstep_order(SalpEnv* h, int mode);
 
 /* GAE / returns over a rollout buffer: stable_baselines3's

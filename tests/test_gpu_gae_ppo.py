@@ -180,3 +180,24 @@ def test_timeout_bootstrap_in_collection():
     ok = ~r.terminated
     assert torch.equal(model.buf.rewards[0][ok], want[ok])
     assert not torch.equal(model.buf.rewards[0][ok], r.reward.float()[ok])
+
+
+def test_collection_is_identical_in_sorted_and_env_order():
+    """PPO collection through salp_step: the sorted lock-step launch order
+    (default at this size) and env order fill identical rollout buffers."""
+    from grasp_lab_salp_amd.ppo import PPO
+    from grasp_lab_salp_amd.vec_env import SalpVecEnv
+    bufs = []
+    for mode in (1, 0):
+        env = SalpVecEnv(4096, seed=9, infos=False)
+        env.sim.set_lockstep_order(mode)
+        model = PPO("MlpPolicy", env, n_steps=6, batch_size=4096, n_epochs=1, seed=5)
+        model.collect_rollouts()
+        torch.cuda.synchronize()
+        b = model.buf
+        bufs.append([getattr(b, k).clone() for k in ("obs", "actions", "rewards", "episode_starts", "values",
+                                                      "log_probs", "advantages", "returns")])
+        assert all(torch.isfinite(t).all() for t in bufs[-1])
+        env.close()
+    for x, y in zip(*bufs):
+        assert torch.equal(x.view(torch.int32), y.view(torch.int32))

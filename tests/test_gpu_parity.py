@@ -317,7 +317,7 @@ def test_sorted_lockstep_order_changes_nothing_but_time(n):
     act = torch.tensor(random_actions(rng, n), device="cuda")
     sa, sb = a.step(act, auto_reset=True), b.step(act, auto_reset=True)
     assert torch.equal(ra.view(torch.int64), rb.view(torch.int64))
-    for x, y in ((sa.obs, sb.obs), (sa.reward, sb.reward), (sa.info, sb.info)):
+    for x, y in ((sa.obs, sb.obs), (sa.reward, sb.reward), (sa.info, sb.info), (sa.terminal_obs, sb.terminal_obs)):
         assert torch.equal(x.contiguous().view(torch.int32 if x.dtype == torch.float32 else torch.int64),
                            y.contiguous().view(torch.int32 if y.dtype == torch.float32 else torch.int64))
     assert torch.equal(sa.terminated, sb.terminated) and torch.equal(sa.truncated, sb.truncated)

@@ -66,6 +66,7 @@ def main():
     ap.add_argument("--iters", type=int, default=2)
     ap.add_argument("--gae-steps", type=int, default=2048)
     ap.add_argument("--trend-iters", type=int, default=0)
+    ap.add_argument("--lockstep-order", type=int, default=-1, help="salp_set_lockstep_order mode")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -77,6 +78,7 @@ def main():
     from grasp_lab_salp_amd.shard import env_id_offset, reduce_run
     from grasp_lab_salp_amd.vec_env import SalpVecEnv
     env = SalpVecEnv(a.n_envs, seed=0, env_id_offset=env_id_offset(rank, a.n_envs), infos=False)
+    env.sim.set_lockstep_order(a.lockstep_order)
     model = PPO("MlpPolicy", env, n_steps=a.n_steps, batch_size=a.batch_size, n_epochs=a.n_epochs, seed=0)
     model.learn(max(1, a.trend_iters) * a.n_steps * a.n_envs)   # warm-up (+ trend) iterations
     trend = list(model.history)
