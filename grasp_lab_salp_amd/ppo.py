@@ -505,7 +505,7 @@ class PPO:
         update to the next went stale after a collection (from the second or
         third update on its replays left all-zero, then NaN, gradients while
         the same minibatch computed eagerly was finite;
-        tools/debug_ppo_drift.py, DESIGN.md §9)."""
+        tools/debug_ppo_drift.py, DESIGN.md §5)."""
         N = self.n_steps * self.n_envs
         self._graph, self._graph_warm = None, 0
         acc = torch.zeros(4, device=self.device)

@@ -201,3 +201,49 @@ def test_collection_is_identical_in_sorted_and_env_order():
         env.close()
     for x, y in zip(*bufs):
         assert torch.equal(x.view(torch.int32), y.view(torch.int32))
+
+
+def test_graphed_update_matches_eager_after_several_collections():
+    """The HIP-graph minibatch step equals the same step run eagerly from the
+    same parameters and Adam state, also in the third update (a graph kept
+    from the first update went stale after collections: zero, then NaN,
+    gradients; tools/debug_ppo_drift.py)."""
+    from grasp_lab_salp_amd.ppo import PPO
+    from grasp_lab_salp_amd.vec_env import SalpVecEnv
+    env = SalpVecEnv(32768, seed=0, infos=False)
+    model = PPO("MlpPolicy", env, n_steps=8, batch_size=32768, n_epochs=2, seed=0, use_graphs=True)
+    seen = []
+    inner = model._graphed_minibatch
+
+    def tensors():
+        out = []
+        for p in model.policy.parameters():
+            out.append(p.data)
+            out += [v for v in model.opt.state.get(p, {}).values() if torch.is_tensor(v)]
+        return out
+
+    def check(idx):
+        if model._graph is None or len(model.history) < 2 or seen:
+            return inner(idx)
+        pre = [t.clone() for t in tensors()]
+        inner(idx)
+        g_graph = [p.grad.clone() for p in model.policy.parameters()]
+        post = [t.clone() for t in tensors()]
+        keep = [p.grad for p in model.policy.parameters()]
+        for t, s in zip(tensors(), pre):
+            t.copy_(s)
+        for p in model.policy.parameters():
+            p.grad = None
+        model._minibatch(model._g_idx, torch.zeros(4, device=model.device))
+        seen.append([torch.equal(a, p.grad) for a, p in zip(g_graph, model.policy.parameters())])
+        for p, g in zip(model.policy.parameters(), keep):
+            p.grad = g
+        for t, s in zip(tensors(), post):
+            t.copy_(s)
+
+    model._graphed_minibatch = check
+    model.learn(3 * 8 * 32768)
+    assert seen and all(seen[0]), seen
+    assert all(torch.isfinite(p).all() for p in model.policy.parameters())
+    assert all(r["vf_loss"] == r["vf_loss"] for r in model.history)
+    env.close()
