@@ -249,6 +249,7 @@ struct Geo {
     double dimx, dimy;            /* width**3, length**3 */
     double speed;                 /* jet speed (V - V_prev) / dt / A_nozzle */
     double rx;                    /* jet moment arm x */
+    double rm, rI0, rI1;          /* refined reciprocals of m, I0, I1 (geo_recips) */
 };
 /* compute_cross_sectional_area_jit (src/geometry.py:67-75): A0 = area[0],
  * A1 = area[1] = area[2]; compute_drag_coefficient_jit (src/geometry.py:
@@ -317,10 +318,19 @@ SD void jet_rates(const Params& P, double V, double pV, double wm, bool g32, boo
     g.mr = b32 ? mr32 : mr64;
     g.speed = b32 ? sp32 : sp64;
 }
+/* The divisors of the dynamics' two divisions (F/m, tau/I): computed with the
+ * geometry, so that a tick whose geometry is kept (steady body) keeps them too
+ * instead of re-running three reciprocal chains. */
+SD void geo_recips(Geo& g) {
+    g.rm = rcp_of(g.m).r;
+    g.rI0 = rcp_of(g.I0).r;
+    g.rI1 = rcp_of(g.I1).r;
+}
 SD Geo make_geo(const Params& P, const Core& c, double L, double W, double V, double pV, bool g32,
                 bool pv32, double wm) {
     Geo g = make_geo_shape(P, c, L, W, wm, g32);
     jet_rates(P, V, pV, wm, g32, pv32, g);
+    geo_recips(g);
     return g;
 }
 
@@ -589,6 +599,23 @@ SD void cycle_bounds(Hot& h) {
     h.b2 = h.b1 + h.coast;
 }
 
+/* --------------------------------------------------- steady body */
+/* Will the next tick's body be the steady one?  In COAST and REST the body is
+ * (init_length, init_width) in float64 (body_lw), 70 % of the ticks under
+ * random actions.  If the previous geometry was computed for that body too,
+ * the next tick's update_properties reproduces it bit for bit, and
+ * tick<STEADY> keeps it instead of recomputing (~43 % of a tick;
+ * profiles/r2_experiments.md r2j).  The phase only moves forward within a
+ * cycle, so a lane steady for one tick stays steady until the cycle ends.
+ * The next phase is COAST or REST iff the next cycle_time exceeds both mx and
+ * mx + jet (update_state's chain in tick): the reference's polynomial gives
+ * small contractions a negative jet (and refill) time, so mx + jet < mx
+ * happens (tests/test_gpu_parity.py::test_steady_body_with_negative_phase_times). */
+SD bool next_tick_steady(const Hot& h, const Params& P) {
+    const double ct = h.ct + DT;
+    return h.L == P.L0 && h.W == P.W0 && !h.g32 && ct > h.b1 && ct > h.mx;
+}
+
 /* --------------------------------------------------- one physics tick */
 /* Robot.step (src/robot.py:670-678): update_dynamics (:854-858) with
  * _newton_equations (:789-823), _euler_equations (:825-851),
@@ -601,12 +628,12 @@ SD void cycle_bounds(Hot& h) {
  * branch that uses it, not at the top of the tick (no register round trip;
  * faster in k_rollout, slower in the lock-step kernels: A/B in
  * profiles/r1f_experiments.md). */
-template <bool REC = false, bool RAND = false, bool LATE32 = false>
+template <bool REC = false, bool RAND = false, bool LATE32 = false, bool STEADY = false>
 SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_t rs = 0) {
     /* this cycle's float32-mode geometry, used at the end if the lane is in
      * that mode (issued first so that the LDS latency hides under the tick) */
     double k32[C32_N];
-    if (!LATE32)
+    if (!LATE32 && !STEADY)
         for (int k = 0; k < C32_N; ++k) k32[k] = c32[k];
     const Geo& g = h.geo;
     const double m = g.m;
@@ -663,7 +690,7 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     double ff0 = acc_x * m, ff1 = acc_y * m, ff2 = acc_z * m;
     /* total force and linear acceleration (src/dynamics.py:5-10) */
     double na0, na1, na2;
-    const Rcp rm = rcp_of(m);
+    const Rcp rm{m, g.rm};
     if (RAND) {   /* + force noise (z: zero) */
         na0 = qdiv(((((jf0 + df0) + af0) + cf0) + nf0) + ff0, rm);
         na1 = qdiv(((((jf1 + df1) + af1) + cf1) + nf1) + ff1, rm);
@@ -700,7 +727,7 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     double amt2 = -((at2 * h.al2 + (h.w0 * atw1 - h.w1 * atw0)) + (h.v0 * amv1 - h.v1 * amv0));
     /* total torque and angular acceleration (src/dynamics.py:13-17) */
     double nal0, nal1, nal2;
-    const Rcp rI0 = rcp_of(I0), rI1 = rcp_of(I1);
+    const Rcp rI0{I0, g.rI0}, rI1{I1, g.rI1};
     if (RAND) {   /* + torque noise (x, y: zero) */
         nal0 = qdiv((((dt0 + ct0) + dft0) + amt0) + 0.0, rI0);
         nal1 = qdiv(((((jt1 + dt1) + ct1) + dft1) + amt1) + 0.0, rI1);
@@ -770,6 +797,22 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     bool f;
     body_lw(P, h.phase, h.ct, h.refill, h.mx, h.c, h.cr, h.rr, h.c32, &h.L, &h.W, &f);
     h.g32 = f;
+    if (STEADY) {
+        /* Steady body (see next_tick_steady): update_properties recomputes
+         * the previous tick's volume, water mass, centre of mass, mass,
+         * inertia and drag coefficients bit for bit, so they are kept; what
+         * depends on the previous tick is evaluated by the expressions below
+         * with the same operands (the volume and centre-of-mass differences
+         * are +0). */
+        const double comr = div_dt(h.com - h.com);
+        h.coma = div_dt(comr - h.comr);
+        h.comr = comr;
+        /* jet_rates with g32 = false: its float64 arm */
+        const double pwm = r32(sel(h.pv32, P.density) * h.pV, h.pv32);
+        h.geo.mr = div_dt(water_mass(P, h.V, false) - pwm);
+        h.geo.speed = qdiv(div_dt(h.V - h.pV), rcp_of(P.nozzle_area));
+        return;
+    }
     /* float64 geometry (bitwise the f = false instance of the shared code),
      * replaced by the cycle's float32 geometry where the lane is in that mode */
     const Core c = core(h.L, h.W, false);
@@ -791,6 +834,7 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     h.com = com;
     h.comr = comr;
     jet_rates(P, V, h.pV, wm, f, h.pv32, ng);
+    geo_recips(ng);
     h.geo = ng;
 }
 
@@ -1385,6 +1429,7 @@ SD void unspill(Hot& h, SpillSlot s, const Params& P, uint64_t env_id) {
         h.geo.m = v[51]; h.geo.mr = v[52]; h.geo.I0 = v[53]; h.geo.I1 = v[54]; h.geo.kc0 = v[55];
         h.geo.kc1 = v[56]; h.geo.ra0 = v[57]; h.geo.ra1 = v[58]; h.geo.dimx = v[59]; h.geo.dimy = v[60];
         h.geo.speed = v[61]; h.geo.rx = v[62];
+        geo_recips(h.geo);
     }
     cycle_bounds(h);
 }

@@ -37,7 +37,18 @@ static_assert(kBlock == salp::LANES, "LDS cache stride is the workgroup size");
 template <bool RAND>
 __device__ __forceinline__ void run_cycle(Hot& h, const Params& P, salp::Cache32 c32) {
     const Params PV = salp::pin_params(P);
-    for (int g = 0; h.ct < h.b2 && g < kMaxTicksPerCycle; ++g) salp::tick<false, RAND>(h, PV, c32);
+    // Full ticks until every lane still ticking has reached the steady body
+    // (COAST / REST after one tick of it), then the rest of the cycle without
+    // the geometry (salp_device.h next_tick_steady).  All lanes of a lock-step
+    // wave start the cycle together, so they usually get there together: about
+    // half of a sorted wave's ticks run the short body.  Lanes that finish
+    // drop out of the vote.
+    int g = 0;
+    for (; h.ct < h.b2 && g < kMaxTicksPerCycle; ++g) {
+        if (__all(salp::next_tick_steady(h, PV))) break;
+        salp::tick<false, RAND>(h, PV, c32);
+    }
+    for (; h.ct < h.b2 && g < kMaxTicksPerCycle; ++g) salp::tick<false, RAND, false, true>(h, PV, c32);
 }
 
 // The loop of Robot.step_through_cycle with record=True (src/robot.py:

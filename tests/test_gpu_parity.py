@@ -347,3 +347,46 @@ def test_state_round_trip_through_the_hbm_layout(n):
     env.set_state(st)
     back = env.get_state().cpu()
     assert torch.equal(back.view(torch.int64), st.view(torch.int64))
+
+
+@pytest.mark.parametrize("n", [1, 128])
+def test_steady_body_with_negative_phase_times(n):
+    """The lock-step kernels run a cycle's COAST/REST ticks without the
+    geometry once every lane of the wave is there (salp_device.h
+    next_tick_steady).  Small contractions give negative refill and jet times
+    (the reference's polynomial), so mx + jet < mx: the first ticks are still
+    REFILL with a contracted body although cycle_time > mx + jet.  Every env
+    of the batch gets such an action (the whole wave votes), 4 env-steps,
+    bit for bit against the oracle; then ordinary actions."""
+    env, o = make_pair(n, seed=21)
+    o.reset()
+    rng = np.random.default_rng(8)
+    for k in range(6):
+        act = random_actions(rng, n)
+        if k < 4:
+            act[:, 0] = rng.uniform(0.0, 0.05, n).astype(np.float32)
+        env.step(torch.tensor(act, device="cuda"), auto_reset=True)
+        o.step(act, auto_reset=True)
+        assert_state_equal(env.get_state(), o.state, f"env-step {k}")
+        if k < 4:   # the case is exercised
+            assert (o.state[FIELD["jet_time"]] < 0).all()
+
+
+@pytest.mark.parametrize("job", [0, 3, 17, 21, 22])
+def test_fixture_episode_actions_on_one_env_bit_exact(job):
+    """The actions of a reference episode (tests/golden/episodes.npz) on a
+    single env, HIP lock-step kernel vs oracle, bit for bit after every
+    env-step.  A one-env wave votes alone on the steady-body switch, so this
+    is where a wrong switch shows (job 3, env-step 24: contraction 0.0022,
+    jet time -0.07 s, turn time 0.016 s, i.e. one REFILL tick after
+    cycle_time > mx + jet)."""
+    d = load_episodes()
+    rows = np.where(d["job_index"] == job)[0]
+    env, o = make_pair(1, seed=job)
+    o.reset()
+    o.state[:] = _cpu(env.get_state())
+    for k, r in enumerate(rows):
+        a = np.asarray(d["action"][r], np.float32)[None]
+        env.step(torch.tensor(a, device="cuda"), auto_reset=False)
+        o.step(a, auto_reset=False)
+        assert_state_equal(env.get_state(), o.state, f"job {job} env-step {k}")
