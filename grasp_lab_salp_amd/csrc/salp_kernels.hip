@@ -8,6 +8,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -318,6 +319,7 @@ struct RolloutArgs {
     Params P;
     int64_t n_chunks;
     int32_t chunk;
+    int32_t steady_q8;   // steady ticks a wave runs per full tick of its chunk budget, x256
     int64_t max_steps;
     SalpRolloutBuffers B;
 };
@@ -338,6 +340,163 @@ __device__ __forceinline__ RolloutArgs fresh_args() {
 // registers in one round of loads, run the epilogue/prologue there, store them
 // back, and everyone reloads its tick state from LDS.  HBM sees each env's
 // state once per launch plus the cold rows of the env-steps that end.
+//
+// Re-seating (SALP_ROLLOUT_RESEAT, the default): the workgroup's 256 envs live
+// in 256 LDS slots, and at every chunk boundary each lane reloads the slot the
+// workgroup hands it instead of its own.  Envs whose body still changes (REFILL,
+// JET, the first COAST tick: salp::next_tick_steady false) go to the first
+// lanes, the steady ones (COAST / REST, 70 % of the ticks) after them, so most
+// waves hold only steady envs and run their chunk on tick<STEADY>, which keeps
+// the geometry (43 % of a tick).  A wave runs full ticks while any of its
+// ticking lanes is unsteady, then steady ticks for the rest of its budget
+// (steady_q8 / 256 steady ticks per full tick left), so that the four waves
+// of a workgroup reach the next boundary at about the same time.  Per-env
+// results do not depend on the lane or the chunk an env runs in.
+#ifndef SALP_ROLLOUT_RESEAT
+#define SALP_ROLLOUT_RESEAT 1
+#endif
+
+// Position of the k-th set bit of the 256-bit mask m[0..3] (k < popcount).
+__device__ __forceinline__ int nth_set_lane(const uint64_t* m, int k) {
+    int base = 0;
+    uint64_t w = m[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int c = __popcll(m[j]);
+        if (k < c) {
+            w = m[j];
+            base = 64 * j;
+            break;
+        }
+        k -= c;
+        base = 64 * (j + 1);
+    }
+    int pos = 0;
+#pragma unroll
+    for (int half = 32; half > 0; half >>= 1) {
+        const uint64_t lo = w & ((1ull << half) - 1ull);
+        const int c = __popcll(lo);
+        if (k >= c) {
+            k -= c;
+            w >>= half;
+            pos += half;
+        } else {
+            w = lo;
+        }
+    }
+    return base + pos;
+}
+
+// Does this env's next tick need the geometry (it ticks and its body is not
+// yet the steady one)?
+__device__ __forceinline__ bool unsteady(const Hot& h, const Params& P, bool active) {
+    return active && h.ct < h.b2 && !salp::next_tick_steady(h, P);
+}
+
+#if SALP_ROLLOUT_RESEAT
+template <bool RAND>
+__global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
+    double* const S = A.S;
+    const Params& P = A.P;
+    const int64_t base = (int64_t)blockIdx.x * blockDim.x;
+    const int lane = (int)threadIdx.x;
+    __shared__ double s_cache32[salp::C32_N * salp::LANES];
+    __shared__ double s_spill[salp::SPILL_N * salp::LANES];
+    __shared__ int64_t s_steps[kBlock];
+    __shared__ uint8_t s_flags[kBlock];              // pending | active << 1, per slot
+    __shared__ int16_t s_slot[2][kBlock];            // slot each lane held (double-buffered)
+    __shared__ uint64_t s_mask[2][kBlock / 64];      // unsteady ballots per wave (double-buffered)
+    int s = lane;                                    // this lane runs env base + s
+    int64_t i = base + s;
+    bool pending = false, active = false;
+    int64_t steps = 0;
+    Hot h{};
+    if (i < P.n) {
+        pending = SF(SALP_F_PENDING) != 0.0;
+        steps = A.B.steps_done ? A.B.steps_done[i] : 0;
+        active = !(A.max_steps > 0 && steps >= A.max_steps);
+        salp::load_hot<RAND>(h, S, P, i);
+        salp::resume_cycle(h, S, P, i);
+        salp::fill_cache32(P, h.c, salp::Cache32{s_cache32 + s});
+    }
+    // slots past the end of the batch hold no env: never active, never stored
+    if (!active) h.b2 = -INFINITY;
+    for (int64_t c = 0;; ++c) {
+        const bool last = c == A.n_chunks;
+        const salp::SpillSlot sp{s_spill + s};
+        // Env-step boundary of the lanes whose cycle ended (or that start one)
+        const bool need = active && (!pending || !(h.ct < h.b2));
+        bool uns = unsteady(h, P, active);
+        salp::spill<RAND>(h, sp);
+        if (need) {
+            const RolloutArgs a = fresh_args();
+            const uint64_t env_id = (uint64_t)(a.P.env_offset + i);
+            salp::ColdRegs<RAND> C;
+            salp::load_cold<RAND>(C, a.S, a.P, i);
+            Hot hb;
+            salp::unspill<RAND>(hb, sp, a.P, env_id);
+            rollout_boundary<RAND>(hb, &C, a.P, i, env_id, pending, active, steps, a.max_steps, a.B,
+                                   salp::Cache32{s_cache32 + s});
+            salp::store_cold<RAND>(C, a.S, a.P, i);
+            salp::spill<RAND>(hb, sp);
+            uns = unsteady(hb, a.P, active);
+        }
+        if (last) {
+            const RolloutArgs a = fresh_args();
+            salp::unspill<RAND>(h, sp, a.P, (uint64_t)(a.P.env_offset + i));
+            if (i < a.P.n) salp::store_hot<RAND>(h, a.S, a.P, i);
+            break;
+        }
+        // Re-seat: lane k of the workgroup takes the k-th env in the order
+        // (unsteady envs by lane, then steady envs by lane).  One barrier; the
+        // double buffers keep the next boundary's writes off this one's reads.
+        const int b = (int)(c & 1);
+        s_steps[s] = steps;
+        s_flags[s] = (uint8_t)((pending ? 1 : 0) | (active ? 2 : 0));
+        s_slot[b][lane] = (int16_t)s;
+        const uint64_t ballot = __ballot(uns);
+        if ((lane & 63) == 0) s_mask[b][lane >> 6] = ballot;
+        __syncthreads();
+        uint64_t m[kBlock / 64];
+        int n_uns = 0;
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; ++w) {
+            m[w] = s_mask[b][w];
+            n_uns += __popcll(m[w]);
+        }
+        int from;
+        if (lane < n_uns) {
+            from = nth_set_lane(m, lane);
+        } else {
+#pragma unroll
+            for (int w = 0; w < kBlock / 64; ++w) m[w] = ~m[w];
+            from = nth_set_lane(m, lane - n_uns);
+        }
+        s = s_slot[b][from];
+        i = base + s;
+        const int fl = s_flags[s];
+        pending = (fl & 1) != 0;
+        active = (fl & 2) != 0;
+        steps = s_steps[s];
+        {
+            const RolloutArgs a = fresh_args();
+            salp::unspill<RAND>(h, salp::SpillSlot{s_spill + s}, a.P, (uint64_t)(a.P.env_offset + i));
+        }
+        if (!active) h.b2 = -INFINITY;   // a finished lane (or an empty slot) ticks no more
+        const salp::Cache32 c32{s_cache32 + s};
+        const Params PV = salp::pin_params(P);
+        int32_t k = 0;
+        for (; k < A.chunk; ++k) {
+            if (__all(!(h.ct < h.b2) || salp::next_tick_steady(h, PV))) break;
+            if (h.ct < h.b2) salp::tick<false, RAND, true>(h, PV, c32);
+        }
+        const int32_t ks = (int32_t)(((int64_t)(A.chunk - k) * A.steady_q8) >> 8);
+        for (int32_t j = 0; j < ks; ++j)
+            if (h.ct < h.b2) salp::tick<false, RAND, true, true>(h, PV, c32);
+    }
+    if (A.B.steps_done && i < P.n) A.B.steps_done[i] = steps;
+}
+#else
 template <bool RAND>
 __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
     double* const S = A.S;
@@ -389,6 +548,7 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
     }
     if (A.B.steps_done) A.B.steps_done[i] = steps;
 }
+#endif
 
 // The ABI's field-major state (state[f * n + i]) <-> the handle's layout
 // (field-major rows + env-major cold block, salp_device.h "state layout").
@@ -551,6 +711,18 @@ int check_hip(SalpEnv* h, hipError_t e, const char* what) {
 int launched(SalpEnv* h, const char* what) { return check_hip(h, hipGetLastError(), what); }
 
 unsigned blocks_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+// k_rollout's steady ticks per full tick of a wave's chunk budget (x256): a
+// steady tick costs ~0.8 of a full one in this kernel (profiles/r2_experiments.md r2l).
+// SALP_STEADY_Q8 overrides it for tuning runs; it changes throughput only.
+int32_t rollout_steady_q8() {
+    static const int32_t q = [] {
+        const char* e = std::getenv("SALP_STEADY_Q8");
+        const long v = e ? std::strtol(e, nullptr, 10) : 0;
+        return (int32_t)(v > 0 && v < (1 << 16) ? v : 320);
+    }();
+    return q;
+}
 
 // Any randomisation switch on: launch the RAND instantiation of the kernels.
 bool randomized(const Params& d) { return d.rand_dyn || d.rand_dist || d.rand_act || d.rand_obs || d.latency; }
@@ -764,7 +936,7 @@ int salp_rollout(SalpEnv* h, int64_t tick_budget, const SalpRolloutBuffers* buf,
     if (b.capacity < 0) return fail(h, SALP_EINVAL, "salp_rollout: capacity < 0");
     int32_t chunk = b.chunk > 0 ? b.chunk : 128;
     int64_t n_chunks = (tick_budget + chunk - 1) / chunk;
-    RolloutArgs args{h->state, h->dp, n_chunks, chunk, b.max_steps, b};
+    RolloutArgs args{h->state, h->dp, n_chunks, chunk, rollout_steady_q8(), b.max_steps, b};
     hipLaunchKernelGGL(randomized(h->dp) ? k_rollout<true> : k_rollout<false>, dim3(blocks_for(h->n)),
                        dim3(kBlock), 0, (hipStream_t)stream, args);
     return launched(h, "k_rollout");

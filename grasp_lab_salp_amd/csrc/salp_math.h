@@ -205,7 +205,11 @@ SM_QUAL int sm_rem_pio2(double x, double* y0, double* y1) {
 }
 SM_QUAL void sm_sincos_p(double x, double* s_out, double* c_out, SmPoly K) {
     int32_t ix = sm_hi(x) & 0x7fffffff;
-    if (ix <= 0x3fe921fb) { /* |x| <= pi/4 */
+    /* |x| <= pi/4, or x is NaN: the kernels return NaN for it as the
+     * reduction would, and a diverged env's NaN angle then does not drag its
+     * whole wave through the reduction path (roll and pitch of every finite
+     * env stay far below pi/4).  +-inf still takes the reduction (NaN). */
+    if (ix <= 0x3fe921fb || x != x) {
         *s_out = sm_ksin_p(x, 0.0, 0, K);
         *c_out = sm_kcos_p(x, 0.0, K);
         return;

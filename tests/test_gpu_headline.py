@@ -5,8 +5,9 @@ workload, src/salp_robot_env.py:196-299 per env-step).  configs[3]: 524 288
 envs sharded 8 ways, i.e. a 65 536-env handle whose global env ids start at
 rank * 65 536 (here the last rank, 7 * 65 536).
 
-* split invariance at full size: one 8 245-tick launch == the same ticks cut
-  into 85 launches of 97 (state, steps_done and rollout buffers, bit for bit);
+* split invariance at full size: one launch running every env to 6 env-steps
+  == the same work cut into 97-tick launches (state, steps_done and rollout
+  buffers, bit for bit);
 * the headline rollout against the C oracle (oracle/salp_oracle.c, pinned to
   the reference by tests/test_oracle_golden.py) on blocks of env ids spread
   over the 65 536, buffers included;
@@ -61,22 +62,26 @@ def _buffers(cap, n, dev="cuda"):
 
 
 def test_headline_rollout_is_split_invariant_at_65536():
-    """One launch of 85 chunks of 97 ticks == 85 launches of one 97-tick chunk
-    (env-steps end and start only at chunk boundaries, so both runs see the
-    same boundaries).  DESIGN.md §4 'Full-size properties' cites this test."""
+    """One launch that runs every env to 6 env-steps == the same work cut into
+    97-tick launches (state, steps_done and rollout buffers, bit for bit).
+    How far an env gets in a launch depends on the scheduling (k_rollout
+    re-seats envs onto lanes every chunk and gives all-steady waves a longer
+    tick budget), what it computes does not.  DESIGN.md §4 cites this test."""
     p = default_params()
-    chunk, launches = 97, 85
+    chunk, steps = 97, 6
     a = BatchedSalpEnv(N, params=p, seed=SEED)
     b = BatchedSalpEnv(N, params=p, seed=SEED)
     ba, bb = _buffers(32, N), _buffers(32, N)
     sa = torch.zeros(N, dtype=torch.int64, device="cuda")
     sb = torch.zeros(N, dtype=torch.int64, device="cuda")
-    a.rollout(chunk * launches, buffers=ba, steps_done=sa, chunk=chunk)
-    for _ in range(launches):
-        b.rollout(chunk, buffers=bb, steps_done=sb, chunk=chunk)
+    a.rollout(20000, buffers=ba, steps_done=sa, chunk=chunk, max_steps=steps)
+    launches = 0
+    while int(sb.min()) < steps and launches < 400:
+        b.rollout(chunk, buffers=bb, steps_done=sb, chunk=chunk, max_steps=steps)
+        launches += 1
     torch.cuda.synchronize()
-    assert int(sa.min()) >= 3, "every env should complete a few env-steps in 8 245 ticks"
-    assert int(sa.max()) < 32, "the 32-slot buffers must not wrap in this test"
+    assert launches > 40, "the cut run should take many launches"
+    assert int(sa.min()) == steps and int(sa.max()) == steps
     assert torch.equal(sa, sb)
     assert _bits_equal(a.get_state(), b.get_state())
     for k in ba:

@@ -218,6 +218,31 @@ def test_rollout_is_split_invariant_and_matches_oracle():
         assert np.array_equal(_cpu(bufs["dones"][t]), dn)
 
 
+@pytest.mark.parametrize("n,chunk", [(1, 128), (63, 16), (300, 128), (700, 7), (1024, 300)])
+def test_rollout_reseating_in_ragged_batches_equals_lockstep(n, chunk):
+    """k_rollout re-seats the envs of a workgroup onto its lanes at every chunk
+    boundary (steady-body envs together).  Ragged batches (empty slots in the
+    last workgroup), tiny and long chunks: the rollout with max_steps k must
+    equal k lock-step env-steps bit for bit, and so the oracle."""
+    p = default_params()
+    k = 5
+    a = BatchedSalpEnv(n, params=p, seed=31)
+    b = BatchedSalpEnv(n, params=p, seed=31)
+    sa = torch.zeros(n, dtype=torch.int64, device="cuda")
+    for _ in range(2000):
+        a.rollout(977, steps_done=sa, max_steps=k, chunk=chunk)
+        if int(sa.min()) >= k:
+            break
+    assert int(sa.min()) == k and int(sa.max()) == k
+    b.step_random(k)
+    ga = _cpu(a.get_state())
+    assert np.array_equal(ga, _cpu(b.get_state()), equal_nan=True)
+    o = orc.Oracle(p, n, seed=31)
+    o.reset()
+    o.step_random(k)
+    assert_state_equal(ga, o.state, f"rollout n={n} chunk={chunk}")
+
+
 def philox_action(seed, env_id, step):
     """sp_action() of salp_philox.h restated in Python for the test."""
     out = orc.philox([step & 0xFFFFFFFF, step >> 32, env_id & 0xFFFFFFFF, 0 | ((env_id >> 32) << 1)],
