@@ -713,13 +713,13 @@ int launched(SalpEnv* h, const char* what) { return check_hip(h, hipGetLastError
 unsigned blocks_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 // k_rollout's steady ticks per full tick of a wave's chunk budget (x256): a
-// steady tick costs ~0.8 of a full one in this kernel (profiles/r2_experiments.md r2l).
+// steady tick costs ~0.8 of a full one in this kernel (profiles/r2_experiments.md r2l-r2o).
 // SALP_STEADY_Q8 overrides it for tuning runs; it changes throughput only.
 int32_t rollout_steady_q8() {
     static const int32_t q = [] {
         const char* e = std::getenv("SALP_STEADY_Q8");
         const long v = e ? std::strtol(e, nullptr, 10) : 0;
-        return (int32_t)(v > 0 && v < (1 << 16) ? v : 320);
+        return (int32_t)(v > 0 && v < (1 << 16) ? v : 360);
     }();
     return q;
 }
