@@ -285,19 +285,36 @@ def main(argv=None):
     diverged = int((~torch.isfinite(st[HOT_FIELDS]).all(0)).sum())
     bad_rows = int((~torch.isfinite(bufs["obs"]).all(-1)).sum())
 
-    # lock-step drop-in path (one env-step per env per launch) for reference
-    lock = None
+    # the drop-in step paths beside the headline:
+    # * lock-step: salp_step_random(1) x 4, one env-step per env per launch on
+    #   k_step_random (a launch lasts as long as the longest cycle of the batch);
+    # * policy-shaped: salp_step with caller-given actions and obs/reward/flag
+    #   outputs, one env-step per launch, as SalpRobotEnv.step / a learner;
+    # * chained k-step: salp_step_random(32), every env runs its 32 env-steps back
+    #   to back on k_rollout (max_steps) and stops (from 32 env-steps per call on).
+    lock = given = chained32 = None
     if not a.no_lockstep:
         env.step_random(1)
         torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        env.step_random(4)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        lock = 4 * n / (e0.elapsed_time(e1) / 1e3)
+
+        def timed(fn):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / 1e3
+
+        lock = 4 * n / timed(lambda: [env.step_random(1) for _ in range(4)])
+        gen = torch.Generator(device=dev).manual_seed(a.seed + 1)
+        acts = [torch.rand((n, 3), device=dev, generator=gen) * torch.tensor([1.0, 1.0, 2.0], device=dev)
+                - torch.tensor([0.0, 0.0, 1.0], device=dev) for _ in range(4)]
+        given = 4 * n / timed(lambda: [env.step(x, auto_reset=True) for x in acts])
+        chained32 = 32 * n / timed(lambda: env.step_random(32))
 
     elapsed, steps_total, kern_ms, lock_total = reduce_run(elapsed, steps_local, kern_ms, lock, device=dev)
+    given_total = reduce_sums([given or 0.0], device=dev)[0] if given is not None else None
+    chained32_total = reduce_sums([chained32 or 0.0], device=dev)[0] if chained32 is not None else None
     diverged_total, bad_rows_total = reduce_sums([diverged, bad_rows], device=dev)
     seen_world = dist.get_world_size() if world > 1 else 1
     if rank != 0:
@@ -340,6 +357,11 @@ def main(argv=None):
                      "note": "algorithmic bytes = env-steps per launch x (2 x 816 B state + 97 B outputs) "
                              "(SURVEY 8(d)); the kernel is fp64-VALU bound (see roofline_valu)"},
         "lockstep_env_steps_per_sec": lock_total,
+        "step_given_actions_env_steps_per_sec": given_total,
+        "step_random32_chained_env_steps_per_sec": chained32_total,
+        "step_paths_note": "lockstep: salp_step_random(1) x4 (k_step_random); given actions: salp_step x4 "
+                           "with obs/reward/flags out (the SalpRobotEnv.step path); chained: salp_step_random(32) "
+                           "on k_rollout with max_steps (each env 32 env-steps back to back)",
         "divergence": {"diverged_envs_at_end": diverged_total, "envs": n * world,
                        "nonfinite_obs_rows_in_buffer": bad_rows_total, "buffer_rows": cap * n * world,
                        "note": "the reference integrator itself diverges for some actions (jet_time < dt); "

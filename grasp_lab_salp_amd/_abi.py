@@ -6,9 +6,23 @@ drift apart silently.
 """
 import ctypes
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 MAX_OBSTACLES = 4
 OBS_DIM_MAX = 6 + 2 * MAX_OBSTACLES
+
+# salp_collect's packed policy (include/salp.h SALP_POLICY_*), offsets in floats
+POLICY_HIDDEN = 64
+POLICY_OFFSETS = {}
+_off = 0
+for _name, _size in (("pi_w1", POLICY_HIDDEN * OBS_DIM_MAX), ("pi_b1", POLICY_HIDDEN),
+                     ("pi_w2", POLICY_HIDDEN * POLICY_HIDDEN), ("pi_b2", POLICY_HIDDEN),
+                     ("act_w", 3 * POLICY_HIDDEN), ("act_b", 3), ("log_std", 3),
+                     ("vf_w1", POLICY_HIDDEN * OBS_DIM_MAX), ("vf_b1", POLICY_HIDDEN),
+                     ("vf_w2", POLICY_HIDDEN * POLICY_HIDDEN), ("vf_b2", POLICY_HIDDEN),
+                     ("val_w", POLICY_HIDDEN), ("val_b", 1)):
+    POLICY_OFFSETS[_name] = (_off, _size)
+    _off += _size
+POLICY_SIZE = _off
 
 
 class SalpParams(ctypes.Structure):

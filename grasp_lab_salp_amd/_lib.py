@@ -35,6 +35,27 @@ class SalpRolloutBuffers(ctypes.Structure):
     ]
 
 
+class SalpPolicyRollout(ctypes.Structure):
+    _fields_ = [
+        ("weights", ctypes.c_void_p),
+        ("noise_seed", ctypes.c_uint64),
+        ("gamma", ctypes.c_double),
+        ("diverged_obs_abs", ctypes.c_double),
+        ("diverged_reward_abs", ctypes.c_double),
+        ("n_steps", ctypes.c_int64),
+        ("obs", ctypes.c_void_p),
+        ("actions", ctypes.c_void_p),
+        ("rewards", ctypes.c_void_p),
+        ("episode_starts", ctypes.c_void_p),
+        ("values", ctypes.c_void_p),
+        ("log_probs", ctypes.c_void_p),
+        ("episode_start", ctypes.c_void_p),
+        ("last_obs", ctypes.c_void_p),
+        ("ep_stats", ctypes.c_void_p),
+        ("diverged", ctypes.c_void_p),
+    ]
+
+
 class SalpTraceBuffer(ctypes.Structure):
     _fields_ = [
         ("max_samples", ctypes.c_int64),
@@ -59,6 +80,7 @@ SIGNATURES = {
     "salp_step": (ctypes.c_int, [_H, _V, _V, _V, _V, _V, ctypes.c_int, _V, _V, _V]),
     "salp_rollout": (ctypes.c_int, [_H, ctypes.c_int64, ctypes.POINTER(SalpRolloutBuffers), _V]),
     "salp_step_random": (ctypes.c_int, [_H, ctypes.c_int32, _V, _V]),
+    "salp_collect": (ctypes.c_int, [_H, ctypes.POINTER(SalpPolicyRollout), _V]),
     "salp_set_lockstep_order": (ctypes.c_int, [_H, ctypes.c_int]),
     "salp_robot_reset": (ctypes.c_int, [_H, _V, _V]),
     "salp_nozzle_set_angles": (ctypes.c_int, [_H, _V, _V]),

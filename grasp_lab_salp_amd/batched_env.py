@@ -11,7 +11,7 @@ import ctypes
 import torch
 
 from . import _lib
-from ._abi import (EPISODE_METRIC_KEYS, FIELD, FIELDS, INFO, INFO_DIM, INFO_KEYS, MAX_OBSTACLES,
+from ._abi import (EPISODE_METRIC_KEYS, FIELD, FIELDS, INFO, INFO_DIM, INFO_KEYS, MAX_OBSTACLES, POLICY_SIZE,
                    NUM_FIELDS, REWARD_COMPONENT_KEYS, TRACE_DIM, SalpParams, default_params)
 
 __all__ = ["BatchedSalpEnv", "StepResult"]
@@ -192,6 +192,43 @@ class BatchedSalpEnv:
         B.chunk = int(chunk)
         self._run(_lib.load().salp_rollout(self._h, int(tick_budget), ctypes.byref(B), self._stream()))
         return steps_done
+
+    def collect(self, weights, n_steps, buffers, episode_start, last_obs, ep_stats, diverged, noise_seed=0,
+                gamma=0.99, diverged_obs_abs=0.0, diverged_reward_abs=0.0):
+        """Policy-in-the-loop collection (salp_collect): every env runs
+        ``n_steps`` env-steps back to back with actions drawn by the packed
+        MlpPolicy ``weights`` (:func:`ppo.pack_policy`) at its env-step
+        boundaries.  ``buffers``: dict of float32 [n_steps, n, ...] tensors
+        obs, actions, rewards, episode_starts, values, log_probs (SB3's
+        RolloutBuffer fields); ``episode_start`` [n] f32 in/out, ``last_obs``
+        [n, obs_dim] out, ``ep_stats`` [2] f64 and ``diverged`` [1] i64
+        accumulated.  See include/salp.h for the exact semantics."""
+        R = _lib.SalpPolicyRollout()
+        w = weights
+        if w.dtype != torch.float32 or w.numel() != POLICY_SIZE or not w.is_contiguous() or w.device != self.device:
+            raise ValueError(f"weights must be a contiguous float32 [{POLICY_SIZE}] tensor on {self.device}")
+        R.weights = w.data_ptr()
+        shapes = {"obs": (n_steps, self.n_envs, self.obs_dim), "actions": (n_steps, self.n_envs, 3),
+                  "rewards": (n_steps, self.n_envs), "episode_starts": (n_steps, self.n_envs),
+                  "values": (n_steps, self.n_envs), "log_probs": (n_steps, self.n_envs)}
+        for k, shp in shapes.items():
+            t = buffers[k]
+            if t.dtype != torch.float32 or tuple(t.shape) != shp or not t.is_contiguous() or t.device != self.device:
+                raise ValueError(f"buffer {k} must be a contiguous float32 tensor of shape {shp} on {self.device}")
+            setattr(R, k, t.data_ptr())
+        for name, t, dt, shp in (("episode_start", episode_start, torch.float32, (self.n_envs,)),
+                                 ("last_obs", last_obs, torch.float32, (self.n_envs, self.obs_dim)),
+                                 ("ep_stats", ep_stats, torch.float64, (2,)),
+                                 ("diverged", diverged, torch.int64, (1,))):
+            if t.dtype != dt or tuple(t.shape) != shp or not t.is_contiguous() or t.device != self.device:
+                raise ValueError(f"{name} must be a contiguous {dt} tensor of shape {shp} on {self.device}")
+            setattr(R, name, t.data_ptr())
+        R.n_steps = int(n_steps)
+        R.noise_seed = int(noise_seed) & 0xFFFFFFFFFFFFFFFF
+        R.gamma = float(gamma)
+        R.diverged_obs_abs = float(diverged_obs_abs)
+        R.diverged_reward_abs = float(diverged_reward_abs)
+        self._run(_lib.load().salp_collect(self._h, ctypes.byref(R), self._stream()))
 
     # ------------------------------------------- Robot / Nozzle level
     # The reference's bare-robot call sequence (src/compare_trajectories.py:

@@ -611,9 +611,16 @@ SD void cycle_bounds(Hot& h) {
  * mx + jet (update_state's chain in tick): the reference's polynomial gives
  * small contractions a negative jet (and refill) time, so mx + jet < mx
  * happens (tests/test_gpu_parity.py::test_steady_body_with_negative_phase_times). */
+/* The first tick of a cycle is always a full one (h.ct > 0): after a reset
+ * the geometry in the state is Robot.reset's, not update_properties' (its
+ * centre of mass differs in the last bits), so "the previous tick computed this
+ * body" only holds once a tick of the cycle has run.  A cycle whose very first
+ * tick is already in COAST/REST (contraction 0: negative refill and jet times)
+ * right after a reset showed it: tests/test_gpu_parity.py::
+ * test_steady_first_tick_after_reset. */
 SD bool next_tick_steady(const Hot& h, const Params& P) {
     const double ct = h.ct + DT;
-    return h.L == P.L0 && h.W == P.W0 && !h.g32 && ct > h.b1 && ct > h.mx;
+    return h.ct > 0.0 && h.L == P.L0 && h.W == P.W0 && !h.g32 && ct > h.b1 && ct > h.mx;
 }
 
 /* --------------------------------------------------- one physics tick */

@@ -254,22 +254,149 @@ __global__ __launch_bounds__(kBlock) void k_predict_ticks(const double* S, Param
 // per env-step.  Per-env results depend only on (seed, env id): how the work
 // is cut into launches and chunks changes nothing but the count of env-steps
 // a launch completes.
-template <bool RAND, class ST>
+// Policy-in-the-loop collection (salp_collect, include/salp.h): the SB3
+// MlpPolicy evaluated per lane at env-step boundaries.  Weights are uniform
+// over the launch, so their loads are scalar loads; the first hidden layer
+// stays in registers and the second is folded into the heads as it is
+// produced (no second activation array).  float32 like the torch policy.
+constexpr int kPH = SALP_POLICY_HIDDEN, kPIN = SALP_OBS_DIM_MAX;
+
+template <int NOUT>
+__device__ __forceinline__ void policy_mlp(const float* __restrict__ w, int w1, int b1, int w2, int b2, int hw,
+                                           int hb, const float* x, float* out) {
+    float h1[kPH];
+#pragma unroll
+    for (int j = 0; j < kPH; ++j) {
+        float acc = w[b1 + j];
+#pragma unroll
+        for (int k = 0; k < kPIN; ++k) acc = fmaf(w[w1 + j * kPIN + k], x[k], acc);
+        h1[j] = tanhf(acc);
+    }
+#pragma unroll
+    for (int c = 0; c < NOUT; ++c) out[c] = 0.0f;
+#pragma unroll 1
+    for (int j = 0; j < kPH; ++j) {
+        float acc = w[b2 + j];
+#pragma unroll
+        for (int k = 0; k < kPH; ++k) acc = fmaf(w[w2 + j * kPH + k], h1[k], acc);
+        const float t = tanhf(acc);
+#pragma unroll
+        for (int c = 0; c < NOUT; ++c) out[c] = fmaf(w[hw + c * kPH + j], t, out[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < NOUT; ++c) out[c] += w[hb + c];
+}
+
+__device__ __forceinline__ void policy_input(const float* o, int obs_dim, float* x) {
+#pragma unroll
+    for (int k = 0; k < kPIN; ++k) x[k] = k < obs_dim ? o[k] : 0.0f;
+}
+
+__device__ __forceinline__ float policy_value(const float* __restrict__ w, const float* x) {
+    float v;
+    policy_mlp<1>(w, SALP_POLICY_VF_W1, SALP_POLICY_VF_B1, SALP_POLICY_VF_W2, SALP_POLICY_VF_B2, SALP_POLICY_VAL_W,
+                  SALP_POLICY_VAL_B, x, &v);
+    return v;
+}
+
+// Three standard normals (Box-Muller on one Philox draw) for the exploration
+// noise of env `env_id` at its env-step `step`.
+#define SP_STREAM_POLICY 7u
+__device__ __forceinline__ void policy_noise(uint64_t seed, uint64_t env_id, uint64_t step, float z[3]) {
+    const sp_u32x4 r = sp_draw(seed, env_id, step, SP_STREAM_POLICY, 0);
+    const double u1 = ((double)r.v[0] + 1.0) * 0x1.0p-32, u3 = ((double)r.v[2] + 1.0) * 0x1.0p-32;
+    const double rad1 = sqrt(-2.0 * sm_log(u1)), rad2 = sqrt(-2.0 * sm_log(u3));
+    double s1, c1, s2, c2;
+    sm_sincos(6.283185307179586 * sp_u01_32(r.v[1]), &s1, &c1);
+    sm_sincos(6.283185307179586 * sp_u01_32(r.v[3]), &s2, &c2);
+    z[0] = (float)(rad1 * c1);
+    z[1] = (float)(rad1 * s1);
+    z[2] = (float)(rad2 * c2);
+}
+
+// The env's action for observation o: a = mean + std z (unclipped, as SB3's
+// buffer holds it), V(o) and log N(a; mean, std) summed over the dims, in the
+// expression order of torch.distributions.Normal.log_prob.
+__device__ __forceinline__ void policy_act(const SalpPolicyRollout& R, int obs_dim, const float* o, uint64_t env_id,
+                                           uint64_t step, float a[3], float* value, float* logp) {
+    const float* __restrict__ w = R.weights;
+    float x[kPIN];
+    policy_input(o, obs_dim, x);
+    float mean[3];
+    policy_mlp<3>(w, SALP_POLICY_PI_W1, SALP_POLICY_PI_B1, SALP_POLICY_PI_W2, SALP_POLICY_PI_B2, SALP_POLICY_ACT_W,
+                  SALP_POLICY_ACT_B, x, mean);
+    *value = policy_value(w, x);
+    float z[3];
+    policy_noise(R.noise_seed, env_id, step, z);
+    float lp = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float ls = w[SALP_POLICY_LOG_STD + c], sd = expf(ls);
+        a[c] = mean[c] + sd * z[c];
+        const float d = a[c] - mean[c];
+        lp += -(d * d) / (2.0f * (sd * sd)) - logf(sd) - 0.91893853320467274f;
+    }
+    *logp = lp;
+}
+
+// torch.clamp(a, low, high): NaN stays NaN
+__device__ __forceinline__ float clamp_box(float a, float lo, float hi) { return a < lo ? lo : (a > hi ? hi : a); }
+
+// Chained random-action rollout, filling the rollout buffer.  Work proceeds in
+// chunks of `chunk` physics ticks: inside a chunk every lane whose cycle is
+// still running ticks (a tight loop over salp::tick only); between chunks the
+// lanes whose cycle ended finish that env-step and start the next one
+// together, so the heavy env-step epilogue runs once per chunk for all lanes
+// that need it instead of once per lane.  A lane idles at most `chunk` ticks
+// per env-step.  Per-env results depend only on (seed, env id): how the work
+// is cut into launches and chunks changes nothing but the count of env-steps
+// a launch completes.  POL: the actions come from the policy of salp_collect
+// and the outputs go to its buffers (R).
+template <bool RAND, bool POL, class ST>
 __device__ __forceinline__ void rollout_boundary(Hot& h, ST S, const Params& P, int64_t i,
                                                  uint64_t env_id, bool& pending, bool& active,
                                                  int64_t& steps, int64_t max_steps,
-                                                 const SalpRolloutBuffers& B, salp::Cache32 c32) {
+                                                 const SalpRolloutBuffers& B, double* reward_sum,
+                                                 const SalpPolicyRollout& R, salp::Cache32 c32) {
     // o: the env's current observation once this boundary has produced one
     // (after a finished step, or the reset obs after an episode end)
     float o[SALP_OBS_DIM_MAX];
     bool have_o = false;
+    float ep_start = 0.0f;   // POL: episode_start of the env's next step, once a step finished here
     // a few rounds so that zero-tick cycles chain without waiting a chunk
     for (int rep = 0; rep < 4; ++rep) {
         const bool fin = active && pending && !(h.ct < h.b2);
         if (fin) {
             SF(SALP_F_STEP_COUNT) = SF(SALP_F_STEP_COUNT) + 1.0;
             salp::StepOut r = salp::finish_step<RAND>(h, S, P, i, o, nullptr);
-            if (B.capacity > 0) {
+            bool reset = r.terminated || r.truncated;
+            if (POL) {
+                // SB3 collect_rollouts + the learner's divergence guard (ppo.py):
+                // o is the terminal observation here, before any reset
+                const size_t row = (size_t)steps * (size_t)P.n + (size_t)i;
+                float rew = (float)r.reward;
+                bool bad = false;
+                if (R.diverged_obs_abs > 0.0) {
+                    bad = !(fabs(r.reward) <= R.diverged_reward_abs);   // NaN too
+                    for (int k = 0; k < P.obs_dim; ++k) bad = bad || !(fabsf(o[k]) <= (float)R.diverged_obs_abs);
+                }
+                if (bad) {
+                    rew = 0.0f;
+                    atomicAdd((unsigned long long*)R.diverged, 1ull);
+                } else if (r.truncated && !r.terminated) {
+                    float x[kPIN];
+                    policy_input(o, P.obs_dim, x);
+                    rew = rew + (float)R.gamma * policy_value(R.weights, x);
+                }
+                if (reset && !bad) {
+                    atomicAdd(&R.ep_stats[0], SF(SALP_F_EP_RETURN));
+                    atomicAdd(&R.ep_stats[1], 1.0);
+                }
+                R.rewards[row] = rew;
+                reset = reset || bad;
+                ep_start = reset ? 1.0f : 0.0f;
+                R.episode_start[i] = ep_start;
+            } else if (B.capacity > 0) {
                 const size_t slot = (size_t)(steps % B.capacity);
                 const size_t row = slot * (size_t)P.n + (size_t)i;
                 if (B.obs)
@@ -282,27 +409,49 @@ __device__ __forceinline__ void rollout_boundary(Hot& h, ST S, const Params& P, 
                 if (B.rewards) B.rewards[row] = (float)r.reward;
                 if (B.dones) B.dones[row] = (uint8_t)((r.terminated ? 1 : 0) | (r.truncated ? 2 : 0));
             }
+            if (reward_sum) reward_sum[i] += r.reward;
             ++steps;
             pending = false;
-            if (r.terminated || r.truncated) salp::reset_env_philox(h, S, P, i, B.obs_before ? o : nullptr);
+            if (reset) salp::reset_env_philox(h, S, P, i, (POL || B.obs_before) ? o : nullptr);
             have_o = true;
-            if (max_steps > 0 && steps >= max_steps) active = false;
+            if (max_steps > 0 && steps >= max_steps) {
+                active = false;
+                if (POL)
+                    for (int k = 0; k < P.obs_dim; ++k) R.last_obs[(size_t)i * P.obs_dim + k] = o[k];
+            }
         }
         const bool beg = active && !pending;
         if (beg) {
-            if (B.obs_before && B.capacity > 0) {
-                // the observation this step's action is taken on: the one just
-                // produced, else (first step after create / reset / set_state)
+            if ((POL || B.obs_before) && !have_o) {
+                // first step after create / reset / set_state / a previous call:
                 // the env's observation as reset() returns it (noise-free)
-                if (!have_o) {
-                    const salp::Rot R = salp::rot_zyx(h.e0, h.e1, h.e2);
-                    salp::observation(h, R, S, P, i, o);
-                }
-                const size_t row = (size_t)(steps % B.capacity) * (size_t)P.n + (size_t)i;
-                for (int k = 0; k < P.obs_dim; ++k) B.obs_before[row * P.obs_dim + k] = o[k];
+                const salp::Rot Rt = salp::rot_zyx(h.e0, h.e1, h.e2);
+                salp::observation(h, Rt, S, P, i, o);
+                have_o = true;
             }
             float a[3];
-            sp_action(P.seed, env_id, (uint64_t)SF(SALP_F_STEP_COUNT), a);
+            if (POL) {
+                if (!fin) ep_start = R.episode_start[i];
+                float raw[3], v, lp;
+                policy_act(R, P.obs_dim, o, env_id, (uint64_t)SF(SALP_F_STEP_COUNT), raw, &v, &lp);
+                const size_t row = (size_t)steps * (size_t)P.n + (size_t)i;
+                for (int k = 0; k < P.obs_dim; ++k) R.obs[row * P.obs_dim + k] = o[k];
+                R.actions[row * 3 + 0] = raw[0];
+                R.actions[row * 3 + 1] = raw[1];
+                R.actions[row * 3 + 2] = raw[2];
+                R.values[row] = v;
+                R.log_probs[row] = lp;
+                R.episode_starts[row] = ep_start;
+                a[0] = clamp_box(raw[0], 0.0f, 1.0f);
+                a[1] = clamp_box(raw[1], 0.0f, 1.0f);
+                a[2] = clamp_box(raw[2], -1.0f, 1.0f);
+            } else {
+                if (B.obs_before && B.capacity > 0) {
+                    const size_t row = (size_t)(steps % B.capacity) * (size_t)P.n + (size_t)i;
+                    for (int k = 0; k < P.obs_dim; ++k) B.obs_before[row * P.obs_dim + k] = o[k];
+                }
+                sp_action(P.seed, env_id, (uint64_t)SF(SALP_F_STEP_COUNT), a);
+            }
             salp::begin_step<RAND>(h, S, P, i, a[0], a[1], a[2], c32);
             pending = true;
         }
@@ -322,6 +471,11 @@ struct RolloutArgs {
     int32_t steady_q8;   // steady ticks a wave runs per full tick of its chunk budget, x256
     int64_t max_steps;
     SalpRolloutBuffers B;
+    double* reward_sum;  // += each finished env-step's reward (salp_step_random), or null
+    int32_t fresh;       // 1: every env starts a new env-step (drops an in-flight cycle), as
+                         // the lock-step kernels do; 0: an in-flight cycle resumes
+    int32_t pad_;
+    SalpPolicyRollout R;  // POL kernels (salp_collect)
 };
 static_assert(sizeof(RolloutArgs) % 8 == 0, "RolloutArgs is copied as 8-byte words");
 typedef const __attribute__((address_space(4))) uint64_t* KernargWords;
@@ -394,7 +548,7 @@ __device__ __forceinline__ bool unsteady(const Hot& h, const Params& P, bool act
 }
 
 #if SALP_ROLLOUT_RESEAT
-template <bool RAND>
+template <bool RAND, bool POL>
 __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
     double* const S = A.S;
     const Params& P = A.P;
@@ -406,13 +560,14 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
     __shared__ uint8_t s_flags[kBlock];              // pending | active << 1, per slot
     __shared__ int16_t s_slot[2][kBlock];            // slot each lane held (double-buffered)
     __shared__ uint64_t s_mask[2][kBlock / 64];      // unsteady ballots per wave (double-buffered)
+    __shared__ uint64_t s_amask[2][kBlock / 64];     // active ballots per wave (double-buffered)
     int s = lane;                                    // this lane runs env base + s
     int64_t i = base + s;
     bool pending = false, active = false;
     int64_t steps = 0;
     Hot h{};
     if (i < P.n) {
-        pending = SF(SALP_F_PENDING) != 0.0;
+        pending = !A.fresh && SF(SALP_F_PENDING) != 0.0;
         steps = A.B.steps_done ? A.B.steps_done[i] : 0;
         active = !(A.max_steps > 0 && steps >= A.max_steps);
         salp::load_hot<RAND>(h, S, P, i);
@@ -421,8 +576,9 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
     }
     // slots past the end of the batch hold no env: never active, never stored
     if (!active) h.b2 = -INFINITY;
+    bool all_done = false;   // no env of the workgroup has an env-step left (max_steps)
     for (int64_t c = 0;; ++c) {
-        const bool last = c == A.n_chunks;
+        const bool last = c == A.n_chunks || all_done;
         const salp::SpillSlot sp{s_spill + s};
         // Env-step boundary of the lanes whose cycle ended (or that start one)
         const bool need = active && (!pending || !(h.ct < h.b2));
@@ -435,8 +591,8 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
             salp::load_cold<RAND>(C, a.S, a.P, i);
             Hot hb;
             salp::unspill<RAND>(hb, sp, a.P, env_id);
-            rollout_boundary<RAND>(hb, &C, a.P, i, env_id, pending, active, steps, a.max_steps, a.B,
-                                   salp::Cache32{s_cache32 + s});
+            rollout_boundary<RAND, POL>(hb, &C, a.P, i, env_id, pending, active, steps, a.max_steps, a.B,
+                                        a.reward_sum, a.R, salp::Cache32{s_cache32 + s});
             salp::store_cold<RAND>(C, a.S, a.P, i);
             salp::spill<RAND>(hb, sp);
             uns = unsteady(hb, a.P, active);
@@ -455,15 +611,22 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
         s_flags[s] = (uint8_t)((pending ? 1 : 0) | (active ? 2 : 0));
         s_slot[b][lane] = (int16_t)s;
         const uint64_t ballot = __ballot(uns);
-        if ((lane & 63) == 0) s_mask[b][lane >> 6] = ballot;
+        const uint64_t aballot = __ballot(active);
+        if ((lane & 63) == 0) {
+            s_mask[b][lane >> 6] = ballot;
+            s_amask[b][lane >> 6] = aballot;
+        }
         __syncthreads();
         uint64_t m[kBlock / 64];
         int n_uns = 0;
+        uint64_t any_active = 0;
 #pragma unroll
         for (int w = 0; w < kBlock / 64; ++w) {
             m[w] = s_mask[b][w];
             n_uns += __popcll(m[w]);
+            any_active |= s_amask[b][w];
         }
+        all_done = any_active == 0;   // the same for every lane of the workgroup
         int from;
         if (lane < n_uns) {
             from = nth_set_lane(m, lane);
@@ -483,6 +646,7 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
             salp::unspill<RAND>(h, salp::SpillSlot{s_spill + s}, a.P, (uint64_t)(a.P.env_offset + i));
         }
         if (!active) h.b2 = -INFINITY;   // a finished lane (or an empty slot) ticks no more
+        if (all_done) continue;          // next pass stores the state and leaves
         const salp::Cache32 c32{s_cache32 + s};
         const Params PV = salp::pin_params(P);
         int32_t k = 0;
@@ -497,13 +661,13 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
     if (A.B.steps_done && i < P.n) A.B.steps_done[i] = steps;
 }
 #else
-template <bool RAND>
+template <bool RAND, bool POL>
 __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
     double* const S = A.S;
     const Params& P = A.P;
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.n) return;
-    bool pending = SF(SALP_F_PENDING) != 0.0;
+    bool pending = !A.fresh && SF(SALP_F_PENDING) != 0.0;
     int64_t steps = A.B.steps_done ? A.B.steps_done[i] : 0;
     bool active = !(A.max_steps > 0 && steps >= A.max_steps);
     LANE_CACHE32();
@@ -517,7 +681,7 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
     for (int64_t c = 0; c <= A.n_chunks; ++c) {
         // Env-step boundary, taken by the whole wave when any lane needs it.
         const bool need = active && (!pending || !(h.ct < h.b2));
-        const bool last = c == A.n_chunks;
+        const bool last = c == A.n_chunks || !__any(active || need);
         if (__any(need) || last) {
             salp::spill<RAND>(h, sp);
             if (need) {
@@ -528,7 +692,8 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
                 salp::load_cold<RAND>(C, a.S, a.P, i);
                 Hot hb;
                 salp::unspill<RAND>(hb, sp, a.P, env_id);
-                rollout_boundary<RAND>(hb, &C, a.P, i, env_id, pending, active, steps, a.max_steps, a.B, c32);
+                rollout_boundary<RAND, POL>(hb, &C, a.P, i, env_id, pending, active, steps, a.max_steps, a.B,
+                                            a.reward_sum, a.R, c32);
                 salp::store_cold<RAND>(C, a.S, a.P, i);
                 salp::spill<RAND>(hb, sp);
             }
@@ -693,6 +858,7 @@ struct SalpEnv {
     int32_t *sort_ids = nullptr, *sort_order = nullptr;
     void* sort_temp = nullptr;
     size_t sort_temp_bytes = 0;
+    int64_t* step_counts = nullptr;   // per-env env-step counter of a chained salp_step_random
 };
 
 namespace {
@@ -829,6 +995,7 @@ int salp_create(const SalpParams* p, int64_t n_envs, uint64_t seed, int64_t env_
         if (!rc) rc = check_hip(nullptr, hipMalloc(&h->sort_ids, sizeof(int32_t) * n_envs), "hipMalloc(sort)");
         if (!rc) rc = check_hip(nullptr, hipMalloc(&h->sort_order, sizeof(int32_t) * n_envs), "hipMalloc(sort)");
         if (!rc) rc = check_hip(nullptr, hipMalloc(&h->sort_temp, tb > 0 ? tb : 1), "hipMalloc(sort)");
+        if (!rc) rc = check_hip(nullptr, hipMalloc(&h->step_counts, sizeof(int64_t) * n_envs), "hipMalloc(steps)");
         h->sort_temp_bytes = tb;
         if (rc) { g_last_error = h->err.empty() ? g_last_error : h->err; salp_destroy(h); return SALP_ENOMEM; }
     }
@@ -849,7 +1016,7 @@ int salp_destroy(SalpEnv* h) {
     if (!h) return SALP_OK;
     (void)hipSetDevice(h->device);
     for (void* p : {(void*)h->state, (void*)h->sort_keys, (void*)h->sort_keys_out, (void*)h->sort_ids,
-                    (void*)h->sort_order, h->sort_temp})
+                    (void*)h->sort_order, h->sort_temp, (void*)h->step_counts})
         if (p) (void)hipFree(p);
     delete h;
     return SALP_OK;
@@ -917,10 +1084,49 @@ int salp_step(SalpEnv* h, const float* actions, float* obs_out, double* reward_o
     return launched(h, "k_step");
 }
 
+// salp_step_random with n_steps >= kChainedMinSteps runs on the chained kernel:
+// every env does its n_steps env-steps back to back and stops (max_steps),
+// instead of the whole wave waiting for its slowest cycle at every env-step.
+// Same per-env results (the actions are keyed by env id and step index either
+// way).  The chained launch lasts as long as the workgroup whose slowest env
+// has the longest sum of n_steps cycles, so it only pays for long calls
+// (65 536 envs, M env-steps/s lock-step / chained: k 4 32.0 / 27.1, k 16
+// 34.9 / 34.8, k 32 35.2 / 37.2; profiles/r2_experiments.md r2q).
+// SALP_STEP_RANDOM_LOCKSTEP=1 keeps the lock-step kernel for every n_steps.
+constexpr int32_t kChainedMinSteps = 32;
+static bool step_random_chained(int32_t n_steps) {
+    static const bool lock = [] {
+        const char* e = std::getenv("SALP_STEP_RANDOM_LOCKSTEP");
+        return e && e[0] == '1';
+    }();
+    return n_steps >= kChainedMinSteps && !lock;
+}
+
 int salp_step_random(SalpEnv* h, int32_t n_steps, double* reward_sum_out, void* stream) {
     if (!h) return fail(nullptr, SALP_EINVAL, "salp_step_random: null handle");
     if (n_steps < 0) return fail(h, SALP_EINVAL, "salp_step_random: n_steps < 0");
     int rc;
+    if (step_random_chained(n_steps)) {
+        hipStream_t st = (hipStream_t)stream;
+        rc = check_hip(h, hipMemsetAsync(h->step_counts, 0, sizeof(int64_t) * h->n, st), "salp_step_random memset");
+        if (!rc && reward_sum_out)
+            rc = check_hip(h, hipMemsetAsync(reward_sum_out, 0, sizeof(double) * h->n, st), "salp_step_random memset");
+        if (rc) return rc;
+        SalpRolloutBuffers b{};
+        b.steps_done = h->step_counts;
+        b.max_steps = n_steps;
+        static const int32_t chunk = [] {   // SALP_STEP_RANDOM_CHUNK: tuning runs only
+            const char* e = std::getenv("SALP_STEP_RANDOM_CHUNK");
+            const long v = e ? std::strtol(e, nullptr, 10) : 0;
+            return (int32_t)(v > 0 && v < 4096 ? v : 128);
+        }();
+        // bound: n_steps cycles of the longest legitimate length (the lock-step guard)
+        const int64_t n_chunks = ((int64_t)n_steps * kMaxTicksPerCycle + chunk - 1) / chunk;
+        RolloutArgs args{h->state, h->dp, n_chunks, chunk, rollout_steady_q8(), n_steps, b, reward_sum_out, 1, 0};
+        hipLaunchKernelGGL((randomized(h->dp) ? k_rollout<true, false> : k_rollout<false, false>), dim3(blocks_for(h->n)),
+                           dim3(kBlock), 0, st, args);
+        return launched(h, "k_rollout(step_random)");
+    }
     const int32_t* order = lockstep_order(h, nullptr, n_steps, stream, &rc);
     if (rc) return rc;
     hipLaunchKernelGGL(randomized(h->dp) ? k_step_random<true> : k_step_random<false>, dim3(blocks_for(h->n)),
@@ -936,10 +1142,32 @@ int salp_rollout(SalpEnv* h, int64_t tick_budget, const SalpRolloutBuffers* buf,
     if (b.capacity < 0) return fail(h, SALP_EINVAL, "salp_rollout: capacity < 0");
     int32_t chunk = b.chunk > 0 ? b.chunk : 128;
     int64_t n_chunks = (tick_budget + chunk - 1) / chunk;
-    RolloutArgs args{h->state, h->dp, n_chunks, chunk, rollout_steady_q8(), b.max_steps, b};
-    hipLaunchKernelGGL(randomized(h->dp) ? k_rollout<true> : k_rollout<false>, dim3(blocks_for(h->n)),
+    RolloutArgs args{h->state, h->dp, n_chunks, chunk, rollout_steady_q8(), b.max_steps, b, nullptr, 0, 0};
+    hipLaunchKernelGGL((randomized(h->dp) ? k_rollout<true, false> : k_rollout<false, false>), dim3(blocks_for(h->n)),
                        dim3(kBlock), 0, (hipStream_t)stream, args);
     return launched(h, "k_rollout");
+}
+
+int salp_collect(SalpEnv* h, const SalpPolicyRollout* r, void* stream) {
+    if (!h) return fail(nullptr, SALP_EINVAL, "salp_collect: null handle");
+    if (!r || !r->weights || r->n_steps <= 0)
+        return fail(h, SALP_EINVAL, "salp_collect: weights and n_steps > 0 are required");
+    if (!r->obs || !r->actions || !r->rewards || !r->episode_starts || !r->values || !r->log_probs ||
+        !r->episode_start || !r->last_obs || !r->ep_stats || !r->diverged)
+        return fail(h, SALP_EINVAL, "salp_collect: every buffer is required");
+    if (r->n_steps > (int64_t)1 << 24) return fail(h, SALP_EINVAL, "salp_collect: n_steps too large");
+    hipStream_t st = (hipStream_t)stream;
+    int rc = check_hip(h, hipMemsetAsync(h->step_counts, 0, sizeof(int64_t) * h->n, st), "salp_collect memset");
+    if (rc) return rc;
+    SalpRolloutBuffers b{};
+    b.steps_done = h->step_counts;
+    b.max_steps = r->n_steps;
+    const int32_t chunk = 128;
+    const int64_t n_chunks = (r->n_steps * kMaxTicksPerCycle + chunk - 1) / chunk;
+    RolloutArgs args{h->state, h->dp, n_chunks, chunk, rollout_steady_q8(), r->n_steps, b, nullptr, 1, 0, *r};
+    hipLaunchKernelGGL((randomized(h->dp) ? k_rollout<true, true> : k_rollout<false, true>), dim3(blocks_for(h->n)),
+                       dim3(kBlock), 0, st, args);
+    return launched(h, "k_rollout(collect)");
 }
 
 int salp_robot_reset(SalpEnv* h, const uint8_t* mask, void* stream) {

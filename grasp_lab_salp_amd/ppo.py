@@ -10,6 +10,10 @@ scan (HIP kernel ``salp_gae``) and the policy all stay in HBM:
   clipped to the action box before the step (SB3 ``collect_rollouts``);
   truncated-not-terminated episodes get ``gamma * V(terminal_obs)`` added to
   their reward (SB3's timeout bootstrap);
+  or, with ``collect="chained"``, ``salp_collect``: the policy is evaluated
+  inside the chained simulation kernel at each env's own env-step boundaries
+  (exploration noise from Philox keyed by env id and step), so no env waits
+  for the slowest cycle of the batch between two steps;
 * advantages / returns: ``salp_gae`` (bit-identical to SB3's NumPy code,
   oracle/gae.py);
 * update: SB3 PPO's clipped surrogate + value MSE - entropy, advantage
@@ -36,7 +40,7 @@ import torch.distributed as dist
 from torch import nn
 
 from . import _lib
-from ._abi import INFO
+from ._abi import INFO, OBS_DIM_MAX, POLICY_OFFSETS, POLICY_SIZE
 
 __all__ = ["compute_gae", "ppo_loss", "torch_ppo_loss", "ActorCritic", "SplitKLinear", "RolloutBuffer", "PPO",
            "allreduce_gradients", "sampling_generator", "timeout_bootstrap", "diverged_mask"]
@@ -224,6 +228,38 @@ class ActorCritic(nn.Module):
         return self.value(obs), d.log_prob(actions).sum(-1), d.entropy().sum(-1)
 
 
+def pack_policy(pol, out=None):
+    """The ActorCritic's parameters in salp_collect's packed float32 layout
+    (include/salp.h SALP_POLICY_*; first-layer inputs zero-padded to
+    OBS_DIM_MAX columns).  ``out``: a preallocated [POLICY_SIZE] tensor."""
+    lin = [m for m in pol.pi_net if isinstance(m, nn.Linear)] + [m for m in pol.vf_net if isinstance(m, nn.Linear)]
+    if len(lin) != 4 or lin[1].in_features != 64 or lin[0].out_features != 64 or lin[0].in_features > OBS_DIM_MAX:
+        raise ValueError("salp_collect runs the 64-64 tanh MlpPolicy only")
+    p = lin[0].weight
+    w = out if out is not None else torch.empty(POLICY_SIZE, dtype=torch.float32, device=p.device)
+    w.zero_()
+
+    def put(name, t):
+        off, size = POLICY_OFFSETS[name]
+        if name.endswith("w1"):
+            w[off:off + size].view(64, OBS_DIM_MAX)[:, :t.shape[1]].copy_(t)
+        else:
+            w[off:off + size].copy_(t.reshape(-1))
+
+    with torch.no_grad():
+        for pre, (l1, l2) in (("pi", lin[:2]), ("vf", lin[2:])):
+            put(pre + "_w1", l1.weight)
+            put(pre + "_b1", l1.bias)
+            put(pre + "_w2", l2.weight)
+            put(pre + "_b2", l2.bias)
+        put("act_w", pol.action_net.weight)
+        put("act_b", pol.action_net.bias)
+        put("log_std", pol.log_std)
+        put("val_w", pol.value_net.weight)
+        put("val_b", pol.value_net.bias)
+    return w
+
+
 def sampling_generator(seed, device):
     """The exploration-noise generator of one rank: seeded with (seed, rank),
     so ranks that share initial weights still draw independent actions for
@@ -307,13 +343,16 @@ class PPO:
     def __init__(self, policy, env, learning_rate=3e-4, n_steps=2048, batch_size=64, n_epochs=10, gamma=0.99,
                  gae_lambda=0.95, clip_range=0.2, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5,
                  normalize_advantage=True, seed=0, device=None, verbose=0, reset_nonfinite=True,
-                 use_graphs=None, fused_loss=None):
+                 use_graphs=None, fused_loss=None, collect="lockstep"):
         if policy not in ("MlpPolicy", None) and not isinstance(policy, nn.Module):
             raise ValueError("policy must be 'MlpPolicy' or an nn.Module")
         if fused_loss and isinstance(policy, nn.Module) and not all(
                 hasattr(policy, k) for k in ("action_net", "pi_net", "log_std", "value")):
             raise ValueError("fused_loss=True needs an ActorCritic-shaped policy (action_net, pi_net, log_std, "
                              "value); pass fused_loss=False for a custom policy")
+        if collect not in ("lockstep", "chained"):
+            raise ValueError("collect must be 'lockstep' or 'chained'")
+        self.collect = collect
         self.env = env
         self.sim = getattr(env, "sim", env)
         self.device = self.sim.device if device is None else torch.device(device)
@@ -362,6 +401,12 @@ class PPO:
         self.high = torch.tensor([1.0, 1.0, 1.0], device=self.device)
         self._obs = None
         self._episode_starts = torch.ones(self.n_envs, dtype=torch.float32, device=self.device)
+        if collect == "chained":
+            if not isinstance(self.policy, ActorCritic):
+                raise ValueError("collect='chained' evaluates the built-in ActorCritic inside the kernel")
+            self._packed = torch.empty(POLICY_SIZE, dtype=torch.float32, device=self.device)
+            self._last_obs = torch.empty((self.n_envs, self.obs_dim), dtype=torch.float32, device=self.device)
+            self._noise_seed = int(seed) + 1_000_003 * (dist.get_rank() if multi else 0)
         self.num_timesteps = 0
         self.logger = {}
         self.timing = {"collect_s": 0.0, "gae_s": 0.0, "train_s": 0.0}
@@ -379,6 +424,8 @@ class PPO:
         if self._obs is None:
             self._obs = sim.reset()
         self._ep_stats.zero_()
+        if self.collect == "chained":
+            return self._collect_chained(ev, stream)
         for t in range(self.n_steps):
             obs = self._obs
             a, v, lp = pol.act(obs, generator=self.sample_gen)
@@ -407,6 +454,29 @@ class PPO:
             self._episode_starts = done.float()
         with torch.no_grad():
             last_values = pol.value(self._obs).contiguous()
+        ev[1].record(stream)
+        compute_gae(b.rewards, b.values, b.episode_starts, last_values, self._episode_starts.contiguous(),
+                    self.gamma, self.gae_lambda, b.advantages, b.returns)
+        ev[2].record(stream)
+        return ev
+
+    def _collect_chained(self, ev, stream):
+        """collect_rollouts on salp_collect: the same buffers, bootstrap and
+        divergence guard, evaluated per env at its own env-step boundaries
+        inside the simulation kernel (include/salp.h)."""
+        b = self.buf
+        w = pack_policy(self.policy, self._packed)
+        guard = self.reset_nonfinite
+        self.sim.collect(w, self.n_steps, {"obs": b.obs, "actions": b.actions, "rewards": b.rewards,
+                                           "episode_starts": b.episode_starts, "values": b.values,
+                                           "log_probs": b.log_probs},
+                         self._episode_starts, self._last_obs, self._ep_stats, self._nonfinite.view(1),
+                         noise_seed=self._noise_seed, gamma=self.gamma,
+                         diverged_obs_abs=DIVERGED_OBS_ABS if guard else 0.0,
+                         diverged_reward_abs=DIVERGED_REWARD_ABS if guard else 0.0)
+        self._obs = self._last_obs
+        with torch.no_grad():
+            last_values = self.policy.value(self._obs).contiguous()
         ev[1].record(stream)
         compute_gae(b.rewards, b.values, b.episode_starts, last_values, self._episode_starts.contiguous(),
                     self.gamma, self.gae_lambda, b.advantages, b.returns)

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define SALP_ABI_VERSION 4
+#define SALP_ABI_VERSION 5
 
 #define SALP_MAX_OBSTACLES 4
 #define SALP_OBS_DIM_MAX (6 + 2 * SALP_MAX_OBSTACLES)
@@ -148,6 +148,71 @@ int salp_rollout(SalpEnv* h, int64_t tick_budget, const SalpRolloutBuffers* buf,
 /* Same random actions, lock-step: every env performs exactly n_steps
  * env-steps (one full cycle each) with auto-reset.  rewards_out [n] = sum. */
 int salp_step_random(SalpEnv* h, int32_t n_steps, double* reward_sum_out, void* stream);
+
+/* ------------------------------------------------ policy-in-the-loop collection
+ * PPO's collect_rollouts (stable-baselines3 OnPolicyAlgorithm.collect_rollouts,
+ * around the env.step calls of the reference's on-policy learner,
+ * src/train_robot_recurrent_ppo.py:65, 85-107) inside the chained kernel: every env
+ * runs `n_steps` env-steps back to back; at each env-step boundary the lane
+ * evaluates the policy on the env's observation and draws its action there, so
+ * no env waits for the slowest cycle of the batch between steps.
+ *
+ * Policy: SB3 MlpPolicy with net_arch pi=[64, 64], vf=[64, 64], tanh, a
+ * state-independent log_std (diagonal Gaussian).  float32 weights packed in
+ * one array (torch nn.Linear weights are [out][in]; the first layer's input
+ * columns are zero-padded to SALP_OBS_DIM_MAX), offsets in floats:          */
+#define SALP_POLICY_HIDDEN 64
+#define SALP_POLICY_PI_W1 0
+#define SALP_POLICY_PI_B1 (SALP_POLICY_PI_W1 + SALP_POLICY_HIDDEN * SALP_OBS_DIM_MAX)
+#define SALP_POLICY_PI_W2 (SALP_POLICY_PI_B1 + SALP_POLICY_HIDDEN)
+#define SALP_POLICY_PI_B2 (SALP_POLICY_PI_W2 + SALP_POLICY_HIDDEN * SALP_POLICY_HIDDEN)
+#define SALP_POLICY_ACT_W (SALP_POLICY_PI_B2 + SALP_POLICY_HIDDEN)       /* [3][64] */
+#define SALP_POLICY_ACT_B (SALP_POLICY_ACT_W + 3 * SALP_POLICY_HIDDEN)   /* [3] */
+#define SALP_POLICY_LOG_STD (SALP_POLICY_ACT_B + 3)                     /* [3] */
+#define SALP_POLICY_VF_W1 (SALP_POLICY_LOG_STD + 3)
+#define SALP_POLICY_VF_B1 (SALP_POLICY_VF_W1 + SALP_POLICY_HIDDEN * SALP_OBS_DIM_MAX)
+#define SALP_POLICY_VF_W2 (SALP_POLICY_VF_B1 + SALP_POLICY_HIDDEN)
+#define SALP_POLICY_VF_B2 (SALP_POLICY_VF_W2 + SALP_POLICY_HIDDEN * SALP_POLICY_HIDDEN)
+#define SALP_POLICY_VAL_W (SALP_POLICY_VF_B2 + SALP_POLICY_HIDDEN)       /* [1][64] */
+#define SALP_POLICY_VAL_B (SALP_POLICY_VAL_W + SALP_POLICY_HIDDEN)       /* [1] */
+#define SALP_POLICY_SIZE (SALP_POLICY_VAL_B + 1)
+
+/* Per env-step of env i, row t (its t-th step of this call):
+ *   obs[t][i]      the observation the action is taken on;
+ *   actions[t][i]  a = mean + exp(log_std) * z, z ~ N(0, 1) from
+ *                  Philox(noise_seed; global env id, step counter); the env
+ *                  receives clamp(a, Box low, Box high) (SB3 clips, buffers a);
+ *   values, log_probs: V(obs), log N(a; mean, std) summed over the 3 dims;
+ *   episode_starts[t][i]: 1 if obs starts an episode (in: episode_start[i]);
+ *   rewards[t][i]  float32 reward; + gamma * V(terminal obs) where the episode
+ *                  was truncated, not terminated (SB3's timeout bootstrap);
+ *                  0 and a fresh episode where the divergence guard fires
+ *                  (|obs| > diverged_obs_abs, |reward| > diverged_reward_abs or
+ *                  non-finite; guard off when diverged_obs_abs <= 0);
+ * then episode_start[i] (next step starts an episode) and last_obs[i] (the obs
+ * after the last step, the reset obs where it ended an episode).
+ * ep_stats[0..1] += (return, 1) per episode that ended by the task's rules;
+ * diverged[0] += envs reset by the guard.  With observation noise on, the
+ * observation at the first step of a call is the noise-free one. */
+typedef struct SalpPolicyRollout {
+    const float* weights;  /* [SALP_POLICY_SIZE] */
+    uint64_t noise_seed;
+    double gamma;
+    double diverged_obs_abs;
+    double diverged_reward_abs;
+    int64_t n_steps;
+    float* obs;            /* [n_steps][n_envs][obs_dim] */
+    float* actions;        /* [n_steps][n_envs][3]        */
+    float* rewards;        /* [n_steps][n_envs]           */
+    float* episode_starts; /* [n_steps][n_envs]           */
+    float* values;         /* [n_steps][n_envs]           */
+    float* log_probs;      /* [n_steps][n_envs]           */
+    float* episode_start;  /* [n_envs] in/out             */
+    float* last_obs;       /* [n_envs][obs_dim] out       */
+    double* ep_stats;      /* [2] accumulated             */
+    int64_t* diverged;     /* [1] accumulated             */
+} SalpPolicyRollout;
+int salp_collect(SalpEnv* h, const SalpPolicyRollout* r, void* stream);
 
 /* Launch order of the lock-step calls (salp_step, salp_step_random): a
  * launch lasts as long as its slowest wave.  mode 1: envs run sorted by the

@@ -75,7 +75,8 @@ def _header_struct_fields(name):
 
 
 @pytest.mark.parametrize("name,cls", [("SalpParams", _abi.SalpParams), ("SalpRolloutBuffers", _lib.SalpRolloutBuffers),
-                                      ("SalpTraceBuffer", _lib.SalpTraceBuffer)])
+                                      ("SalpTraceBuffer", _lib.SalpTraceBuffer),
+                                      ("SalpPolicyRollout", _lib.SalpPolicyRollout)])
 def test_struct_layouts_match_header(name, cls):
     """The ctypes mirrors declare the header's fields in the header's order."""
     assert _header_struct_fields(name) == [f for f, _ in cls._fields_]

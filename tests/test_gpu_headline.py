@@ -11,7 +11,8 @@ rank * 65 536 (here the last rank, 7 * 65 536).
 * the headline rollout against the C oracle (oracle/salp_oracle.c, pinned to
   the reference by tests/test_oracle_golden.py) on blocks of env ids spread
   over the 65 536, buffers included;
-* the lock-step kernel on ALL 65 536 envs against the OpenMP oracle;
+* the lock-step kernel on ALL 65 536 envs against the OpenMP oracle, and the
+  chained salp_step_random(32) against 32 lock-step calls;
 * the config-4 shard (global ids up to 2^19 - 1, plus a block across 2^32 for
   the Philox counter's high word) against the oracle at the same global ids.
 """
@@ -141,17 +142,41 @@ def test_headline_rollout_matches_oracle_on_blocks():
 
 
 def test_headline_lockstep_all_envs_match_openmp_oracle():
-    """k_step_random on every one of the 65 536 envs, 2 env-steps, against
-    the whole-batch OpenMP oracle (bit for bit: state and reward sums)."""
+    """Every one of the 65 536 envs, 2 random env-steps, against the
+    whole-batch OpenMP oracle (bit for bit: state and reward sums): the
+    lock-step kernel k_step_random (one env-step per call, and two per call).
+    Then the chained salp_step_random(32) (k_rollout with max_steps, every env
+    running its env-steps back to back) equals 32 lock-step calls bit for bit."""
     p = default_params()
     env = BatchedSalpEnv(N, params=p, seed=SEED)
-    rs = env.step_random(2)
+    rs = env.step_random(1)
+    rs = rs + env.step_random(1)
+    two = BatchedSalpEnv(N, params=p, seed=SEED)
+    rs2 = two.step_random(2)
     o = orc.Oracle(p, N, seed=SEED)
     o.reset()
     rs_o, ticks = o.step_random(2, threads=_threads())
     assert ticks > 0
     assert np.array_equal(_cpu(rs), rs_o, equal_nan=True)
     assert_state_equal(env.get_state(), o.state, "lock-step 65536")
+    assert np.array_equal(_cpu(rs2), _cpu(rs), equal_nan=True)   # NaN payloads of a diverged env's sum may differ
+    assert _bits_equal(two.get_state(), env.get_state())
+    rs_c = two.step_random(32)
+    rs_l = torch.zeros_like(rs_c)
+    for _ in range(32):
+        rs_l = rs_l + env.step_random(1)
+    assert np.array_equal(_cpu(rs_c), _cpu(rs_l), equal_nan=True)
+    _equal_up_to_nan_payload(two.get_state(), env.get_state())
+
+
+def _equal_up_to_nan_payload(x, y):
+    """Bit for bit, except that where both hold a NaN the payloads may differ
+    (a diverged env's NaN state goes through different instruction sequences
+    in the chained and the lock-step kernels)."""
+    a, b = _cpu(x), _cpu(y)
+    both_nan = np.isnan(a) & np.isnan(b)
+    diff = (a.view(np.int64) != b.view(np.int64)) & ~both_nan
+    assert not diff.any(), (np.nonzero(diff.any(1))[0].tolist(), int(diff.sum()))
 
 
 @pytest.mark.parametrize("base", [7 * N, (1 << 32) - N // 2])

@@ -167,6 +167,55 @@ def test_step_random_matches_oracle():
     assert_state_equal(env.get_state(), o.state, "step_random")
 
 
+@pytest.mark.parametrize("n", [1, 64, 300])
+def test_steady_first_tick_after_reset(n):
+    """Contraction exactly 0 (a clipped policy action): refill and jet times
+    are negative, so the cycle's very first tick is already COAST.  Right
+    after a reset the state's geometry is Robot.reset's, whose centre of mass
+    differs from update_properties' in the last bits: the steady-body loop
+    must not keep it (found by tests/test_gpu_collect.py, env 79 of a
+    300-env collection).  One env per wave included (n = 1: the lane alone
+    decides the steady switch).  Lock-step step and the chained rollout
+    path, bit for bit against the oracle."""
+    env, o = make_pair(n, seed=5)
+    o.reset()
+    env.set_state(torch.tensor(o.state))
+    rng = np.random.default_rng(7)
+    a = random_actions(rng, n)
+    a[:, 0] = 0.0
+    for t in range(3):
+        r = env.step(torch.tensor(a), auto_reset=True)
+        ro = o.step(a, auto_reset=True)
+        assert np.array_equal(_cpu(r.obs), ro["obs"], equal_nan=True), t
+        assert_state_equal(env.get_state(), o.state, f"contraction 0, step {t}")
+        env.reset()
+        o.reset()
+        env.set_state(torch.tensor(o.state))
+
+
+@pytest.mark.parametrize("n,k", [(300, 32), (2048, 33)])
+def test_chained_step_random_equals_lockstep_steps(n, k):
+    """salp_step_random(k >= 32) runs on the chained kernel (each env does its k
+    env-steps back to back); k calls of salp_step_random(1) run the lock-step
+    kernel.  Same state and reward sums bit for bit, also when the handle
+    holds cycles cut in flight by a tick-budget rollout (both drop them and
+    start a new env-step, as SalpRobotEnv.step would)."""
+    p = default_params()
+    a = BatchedSalpEnv(n, params=p, seed=41)
+    b = BatchedSalpEnv(n, params=p, seed=41)
+    for e in (a, b):
+        e.rollout(333)   # leaves most envs mid-cycle (pending)
+    pend = _cpu(a.field("pending"))
+    assert pend.mean() > 0.5
+    ra = a.step_random(k)
+    rb = torch.zeros_like(ra)
+    for _ in range(k):
+        rb = rb + b.step_random(1)
+    assert np.array_equal(_cpu(ra), _cpu(rb), equal_nan=True)
+    assert torch.equal(a.get_state().view(torch.int64), b.get_state().view(torch.int64))
+    assert np.all(_cpu(a.field("pending")) == 0)
+
+
 def test_rollout_is_split_invariant_and_matches_oracle():
     """Tick-budget rollouts: cutting the same work into different launches gives
     identical bits, equal to the lock-step oracle at env-step boundaries, and
