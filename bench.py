@@ -73,7 +73,11 @@ def pmc_profile(n, budget, chunk):
             s = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if s.get("config") == {"n_envs": n, "tick_budget": budget, "chunk": chunk}:
+        # the latest summary of this configuration that holds the traffic passes
+        # (FETCH_SIZE / WRITE_SIZE) and the fp64 instruction mix
+        d = s.get("derived", {})
+        if (s.get("config") == {"n_envs": n, "tick_budget": budget, "chunk": chunk}
+                and d.get("hbm_bytes") and d.get("fp64_flops")):
             best = (os.path.basename(path), s)
     return best
 
