@@ -260,9 +260,15 @@ __global__ __launch_bounds__(kBlock) void k_predict_ticks(const double* S, Param
 // stays in registers and the second is folded into the heads as it is
 // produced (no second activation array).  float32 like the torch policy.
 constexpr int kPH = SALP_POLICY_HIDDEN, kPIN = SALP_OBS_DIM_MAX;
+// The weights are read through the constant address space: the kernel writes
+// global memory through other pointers, so a generic pointer's uniform loads
+// would be vector loads (one latency-bound load round per hidden unit); from
+// address space 4 they are scalar loads into SGPR operands (collect 18.8 ->
+// 26.7 M env-steps/s at 65 536 envs, profiles/r2_experiments.md r2u).
+typedef const __attribute__((address_space(4))) float* PolicyW;
 
 template <int NOUT>
-__device__ __forceinline__ void policy_mlp(const float* __restrict__ w, int w1, int b1, int w2, int b2, int hw,
+__device__ __forceinline__ void policy_mlp(PolicyW w, int w1, int b1, int w2, int b2, int hw,
                                            int hb, const float* x, float* out) {
     float h1[kPH];
 #pragma unroll
@@ -292,7 +298,7 @@ __device__ __forceinline__ void policy_input(const float* o, int obs_dim, float*
     for (int k = 0; k < kPIN; ++k) x[k] = k < obs_dim ? o[k] : 0.0f;
 }
 
-__device__ __forceinline__ float policy_value(const float* __restrict__ w, const float* x) {
+__device__ __forceinline__ float policy_value(PolicyW w, const float* x) {
     float v;
     policy_mlp<1>(w, SALP_POLICY_VF_W1, SALP_POLICY_VF_B1, SALP_POLICY_VF_W2, SALP_POLICY_VF_B2, SALP_POLICY_VAL_W,
                   SALP_POLICY_VAL_B, x, &v);
@@ -319,7 +325,7 @@ __device__ __forceinline__ void policy_noise(uint64_t seed, uint64_t env_id, uin
 // expression order of torch.distributions.Normal.log_prob.
 __device__ __forceinline__ void policy_act(const SalpPolicyRollout& R, int obs_dim, const float* o, uint64_t env_id,
                                            uint64_t step, float a[3], float* value, float* logp) {
-    const float* __restrict__ w = R.weights;
+    const PolicyW w = (PolicyW)R.weights;
     float x[kPIN];
     policy_input(o, obs_dim, x);
     float mean[3];
@@ -386,7 +392,7 @@ __device__ __forceinline__ void rollout_boundary(Hot& h, ST S, const Params& P, 
                 } else if (r.truncated && !r.terminated) {
                     float x[kPIN];
                     policy_input(o, P.obs_dim, x);
-                    rew = rew + (float)R.gamma * policy_value(R.weights, x);
+                    rew = rew + (float)R.gamma * policy_value((PolicyW)R.weights, x);
                 }
                 if (reset && !bad) {
                     atomicAdd(&R.ep_stats[0], SF(SALP_F_EP_RETURN));

@@ -23,5 +23,5 @@ fi
 step bench 400 python -u bench.py ${BENCH_ARGS}
 if [ -z "$SKIP_PROF" ]; then
     step prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/${TAG}_prof" -o run \
-        -- python3 bench.py --no-cpu-baseline ${PROF_ARGS}
+        -- python3 bench.py --no-cpu-baseline ${PROF_ARGS:---no-lockstep}
 fi
