@@ -811,13 +811,20 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
          * depends on the previous tick is evaluated by the expressions below
          * with the same operands (the volume and centre-of-mass differences
          * are +0). */
-        const double comr = div_dt(h.com - h.com);
-        h.coma = div_dt(comr - h.comr);
-        h.comr = comr;
-        /* jet_rates with g32 = false: its float64 arm */
-        const double pwm = r32(sel(h.pv32, P.density) * h.pV, h.pv32);
-        h.geo.mr = div_dt(water_mass(P, h.V, false) - pwm);
-        h.geo.speed = qdiv(div_dt(h.V - h.pV), rcp_of(P.nozzle_area));
+        /* From the second steady tick on these are all +0 and recompute as +0
+         * (V == pV, pv32 == false, com - com = +0, and div_dt / qdiv of +0 is
+         * +0), so a wave whose lanes are all there skips them. */
+        const bool settled = (__double_as_longlong(h.comr) | __double_as_longlong(h.coma) |
+                              __double_as_longlong(h.geo.mr) | __double_as_longlong(h.geo.speed)) == 0;
+        if (!__all(settled)) {
+            const double comr = div_dt(h.com - h.com);
+            h.coma = div_dt(comr - h.comr);
+            h.comr = comr;
+            /* jet_rates with g32 = false: its float64 arm */
+            const double pwm = r32(sel(h.pv32, P.density) * h.pV, h.pv32);
+            h.geo.mr = div_dt(water_mass(P, h.V, false) - pwm);
+            h.geo.speed = qdiv(div_dt(h.V - h.pV), rcp_of(P.nozzle_area));
+        }
         return;
     }
     /* float64 geometry (bitwise the f = false instance of the shared code),
