@@ -1168,7 +1168,16 @@ int salp_collect(SalpEnv* h, const SalpPolicyRollout* r, void* stream) {
     SalpRolloutBuffers b{};
     b.steps_done = h->step_counts;
     b.max_steps = r->n_steps;
-    const int32_t chunk = 128;
+    // Longer chunks than the rollout's 128: every wave evaluates the policy at
+    // most once per chunk, and that evaluation is on its critical path
+    // (65 536 envs, M env-steps/s by chunk 128 / 192 / 256 / 384 / 512 / 768:
+    // 26.3 / 28.3 / 28.3 / 29.2 / 28.6 / 24.6; profiles/r2_experiments.md r2x).
+    // SALP_COLLECT_CHUNK overrides it for tuning runs.
+    static const int32_t chunk = [] {
+        const char* e = std::getenv("SALP_COLLECT_CHUNK");
+        const long v = e ? std::strtol(e, nullptr, 10) : 0;
+        return (int32_t)(v > 0 && v < 4096 ? v : 384);
+    }();
     const int64_t n_chunks = (r->n_steps * kMaxTicksPerCycle + chunk - 1) / chunk;
     RolloutArgs args{h->state, h->dp, n_chunks, chunk, rollout_steady_q8(), r->n_steps, b, nullptr, 1, 0, *r};
     hipLaunchKernelGGL((randomized(h->dp) ? k_rollout<true, true> : k_rollout<false, true>), dim3(blocks_for(h->n)),
