@@ -85,3 +85,21 @@ def test_struct_layouts_match_header(name, cls):
 def test_abi_version(lib):
     assert lib.salp_abi_version() == _abi.ABI_VERSION
     assert f"#define SALP_ABI_VERSION {_abi.ABI_VERSION}" in open(HEADER).read()
+
+
+def test_policy_layout_matches_header(tmp_path):
+    """salp_collect's packed policy: the SALP_POLICY_* offsets of the header
+    (compiled with gcc) equal grasp_lab_salp_amd._abi.POLICY_OFFSETS, which
+    ppo.pack_policy writes."""
+    import subprocess
+    names = ["PI_W1", "PI_B1", "PI_W2", "PI_B2", "ACT_W", "ACT_B", "LOG_STD", "VF_W1", "VF_B1", "VF_W2", "VF_B2",
+             "VAL_W", "VAL_B", "SIZE"]
+    src = tmp_path / "p.c"
+    src.write_text('#include <stdio.h>\n#include "salp.h"\nint main(void) {\n'
+                   + "".join(f'    printf("%d\\n", (int)(SALP_POLICY_{n}));\n' for n in names) + "    return 0;\n}\n")
+    exe = tmp_path / "p"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    want = [_abi.POLICY_OFFSETS[n.lower()][0] for n in names[:-1]] + [_abi.POLICY_SIZE]
+    assert got == want
+    assert _abi.POLICY_OFFSETS["pi_w1"][1] == _abi.POLICY_HIDDEN * _abi.OBS_DIM_MAX

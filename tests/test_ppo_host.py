@@ -44,3 +44,34 @@ def test_act_with_generator_is_mean_plus_std_noise():
     eps = torch.randn(4, 3, generator=g2)
     assert torch.allclose(a, d.mean + d.stddev * eps)
     assert torch.allclose(lp, d.log_prob(a).sum(-1))
+
+
+def test_pack_policy_layout():
+    """ppo.pack_policy writes the ActorCritic into salp_collect's layout
+    (include/salp.h SALP_POLICY_*): first-layer columns zero-padded to
+    OBS_DIM_MAX, every other tensor flattened [out][in] at its offset."""
+    import torch
+
+    from grasp_lab_salp_amd._abi import OBS_DIM_MAX, POLICY_OFFSETS, POLICY_SIZE
+    from grasp_lab_salp_amd.ppo import ActorCritic, pack_policy
+    torch.manual_seed(0)
+    pol = ActorCritic(10, 3)
+    with torch.no_grad():
+        pol.log_std.copy_(torch.tensor([0.1, -0.2, 0.3]))
+    w = pack_policy(pol)
+    assert w.shape == (POLICY_SIZE,) and w.dtype == torch.float32
+
+    def part(name):
+        off, size = POLICY_OFFSETS[name]
+        return w[off:off + size]
+
+    w1 = part("pi_w1").view(64, OBS_DIM_MAX)
+    assert torch.equal(w1[:, :10], pol.pi_net[0].weight) and not w1[:, 10:].any()
+    assert torch.equal(part("vf_w1").view(64, OBS_DIM_MAX)[:, :10], pol.vf_net[0].weight)
+    assert torch.equal(part("pi_w2").view(64, 64), pol.pi_net[2].weight)
+    assert torch.equal(part("vf_b2"), pol.vf_net[2].bias)
+    assert torch.equal(part("act_w").view(3, 64), pol.action_net.weight)
+    assert torch.equal(part("act_b"), pol.action_net.bias)
+    assert torch.equal(part("log_std"), pol.log_std.detach())
+    assert torch.equal(part("val_w"), pol.value_net.weight.view(-1))
+    assert torch.equal(part("val_b"), pol.value_net.bias)
