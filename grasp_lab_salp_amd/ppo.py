@@ -10,7 +10,7 @@ scan (HIP kernel ``salp_gae``) and the policy all stay in HBM:
   clipped to the action box before the step (SB3 ``collect_rollouts``);
   truncated-not-terminated episodes get ``gamma * V(terminal_obs)`` added to
   their reward (SB3's timeout bootstrap);
-  or, with ``collect="chained"``, ``salp_collect``: the policy is evaluated
+  or, with ``collect="chained"`` (the default from n_steps 256 on), ``salp_collect``: the policy is evaluated
   inside the chained simulation kernel at each env's own env-step boundaries
   (exploration noise from Philox keyed by env id and step), so no env waits
   for the slowest cycle of the batch between two steps;
@@ -343,16 +343,15 @@ class PPO:
     def __init__(self, policy, env, learning_rate=3e-4, n_steps=2048, batch_size=64, n_epochs=10, gamma=0.99,
                  gae_lambda=0.95, clip_range=0.2, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5,
                  normalize_advantage=True, seed=0, device=None, verbose=0, reset_nonfinite=True,
-                 use_graphs=None, fused_loss=None, collect="lockstep"):
+                 use_graphs=None, fused_loss=None, collect="auto"):
         if policy not in ("MlpPolicy", None) and not isinstance(policy, nn.Module):
             raise ValueError("policy must be 'MlpPolicy' or an nn.Module")
         if fused_loss and isinstance(policy, nn.Module) and not all(
                 hasattr(policy, k) for k in ("action_net", "pi_net", "log_std", "value")):
             raise ValueError("fused_loss=True needs an ActorCritic-shaped policy (action_net, pi_net, log_std, "
                              "value); pass fused_loss=False for a custom policy")
-        if collect not in ("lockstep", "chained"):
-            raise ValueError("collect must be 'lockstep' or 'chained'")
-        self.collect = collect
+        if collect not in ("auto", "lockstep", "chained"):
+            raise ValueError("collect must be 'auto', 'lockstep' or 'chained'")
         self.env = env
         self.sim = getattr(env, "sim", env)
         self.device = self.sim.device if device is None else torch.device(device)
@@ -401,6 +400,13 @@ class PPO:
         self.high = torch.tensor([1.0, 1.0, 1.0], device=self.device)
         self._obs = None
         self._episode_starts = torch.ones(self.n_envs, dtype=torch.float32, device=self.device)
+        # auto: the in-kernel collection for the built-in policy on a GPU from
+        # 256 env-steps per collection on (config 5 at n_steps 2048: collection
+        # 5.76 -> 4.21 s; at n_steps 32 the two take the same time)
+        if collect == "auto":
+            collect = ("chained" if self.device.type == "cuda" and isinstance(self.policy, ActorCritic)
+                       and self.n_steps >= 256 else "lockstep")
+        self.collect = collect
         if collect == "chained":
             if not isinstance(self.policy, ActorCritic):
                 raise ValueError("collect='chained' evaluates the built-in ActorCritic inside the kernel")

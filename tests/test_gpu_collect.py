@@ -147,3 +147,11 @@ def test_ppo_with_chained_collection_learns_finite():
             if isinstance(v, float):
                 assert np.isfinite(v), (k, v)
     assert torch.isfinite(model.buf.advantages).all()
+
+
+def test_ppo_collect_auto_choice():
+    """collect='auto': the in-kernel collection from n_steps 256 on (the
+    reference's n_steps is 2048), lock-step below."""
+    venv = SalpVecEnv(256, seed=1)
+    assert PPO("MlpPolicy", venv, n_steps=256, batch_size=256, seed=0).collect == "chained"
+    assert PPO("MlpPolicy", venv, n_steps=32, batch_size=256, seed=0).collect == "lockstep"

@@ -67,7 +67,7 @@ def main():
     ap.add_argument("--gae-steps", type=int, default=2048)
     ap.add_argument("--trend-iters", type=int, default=0)
     ap.add_argument("--lockstep-order", type=int, default=-1, help="salp_set_lockstep_order mode")
-    ap.add_argument("--collect", default="lockstep", choices=("lockstep", "chained"),
+    ap.add_argument("--collect", default="auto", choices=("auto", "lockstep", "chained"),
                     help="collection: salp_step per env-step, or salp_collect (policy inside the kernel)")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -100,7 +100,7 @@ def main():
     if rank == 0:
         res = {"metric": "PPO env-steps/sec (collect + GAE + update), config 5", "value": steps / el,
                "unit": "env-steps/s", "n_gpus": world, "n_envs_per_gpu": a.n_envs, "n_steps": a.n_steps,
-               "batch_size": a.batch_size, "n_epochs": a.n_epochs, "iters": a.iters, "collect": a.collect,
+               "batch_size": a.batch_size, "n_epochs": a.n_epochs, "iters": a.iters, "collect": model.collect,
                "timing_s": model.timing, "losses": model.logger,
                "history": model.history[h0:], "trend": trend if a.trend_iters else None,
                "diverged_envs_reset": model.nonfinite_resets,
