@@ -95,6 +95,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-lockstep", action="store_true")
+    ap.add_argument("--no-parity-check", action="store_true",
+                    help="skip the sampled oracle replay after the timed region")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher + reductions only, gloo on the CPU, no GPU kernels")
     return ap.parse_args(argv)
@@ -265,6 +267,8 @@ def main(argv=None):
     barrier()
     torch.cuda.synchronize()
     s0 = int(done.sum())
+    done0 = done.clone()
+    finite0 = torch.isfinite(env.get_state()[HOT_FIELDS]).all(0)
     # HIP events on the stream the kernel is launched on (torch's current stream)
     stream = torch.cuda.current_stream(dev)
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps)]
@@ -286,8 +290,28 @@ def main(argv=None):
     # the end of the run, and the non-finite observations among the last
     # `cap` env-steps of every env held in the rollout buffer.
     st = env.get_state()
-    diverged = int((~torch.isfinite(st[HOT_FIELDS]).all(0)).sum())
+    finite1 = torch.isfinite(st[HOT_FIELDS]).all(0)
+    diverged = int((~finite1).sum())
     bad_rows = int((~torch.isfinite(bufs["obs"]).all(-1)).sum())
+    # env-steps of the envs whose kinematic state was finite at both ends of
+    # the timed region (an env that diverges stays NaN until its 500-cycle
+    # timeout, longer than the timed region)
+    finite_steps = int(((done - done0) * (finite0 & finite1)).sum())
+
+    # Parity at the bench's own horizon (the checker, after the timed region):
+    # sampled env ids replayed from creation on the C oracle for exactly the
+    # env-steps each completed plus its in-flight cycle; state and the last
+    # `cap` buffer rows compared bit for bit (oracle/sampled.py).
+    parity = None
+    if rank == 0 and not a.no_parity_check:
+        from oracle import sampled
+        t_chk = time.perf_counter()
+        parity = sampled.check(st.cpu().numpy(), done.cpu().numpy(), {k: v.cpu().numpy() for k, v in bufs.items()},
+                               default_params(), a.seed, env_offset=env_id_offset(rank, n), threads=cpu_threads(),
+                               n_random=128)
+        parity["seconds"] = time.perf_counter() - t_chk
+        parity["what"] = ("rank 0's sampled envs (first and last workgroup, diverged envs, random ids) replayed "
+                          "from creation on the C oracle; state + last buffer rows bit for bit")
 
     # the drop-in step paths beside the headline:
     # * lock-step: salp_step_random(1) x 4, one env-step per env per launch on
@@ -319,7 +343,7 @@ def main(argv=None):
     elapsed, steps_total, kern_ms, lock_total = reduce_run(elapsed, steps_local, kern_ms, lock, device=dev)
     given_total = reduce_sums([given or 0.0], device=dev)[0] if given is not None else None
     chained32_total = reduce_sums([chained32 or 0.0], device=dev)[0] if chained32 is not None else None
-    diverged_total, bad_rows_total = reduce_sums([diverged, bad_rows], device=dev)
+    diverged_total, bad_rows_total, finite_total = reduce_sums([diverged, bad_rows, finite_steps], device=dev)
     seen_world = dist.get_world_size() if world > 1 else 1
     if rank != 0:
         dist.destroy_process_group()
@@ -349,7 +373,12 @@ def main(argv=None):
                                "canonical make_env robot (src/train_robot.py:11-21), 2 obstacles",
                    "n_envs_per_gpu": n, "tick_budget": a.tick_budget, "chunk": a.chunk, "rollout_capacity": cap,
                    "parallelism": f"env-shard x{world}"},
-        "ticks_per_sec": steps_total * MEAN_TICKS_PER_ENV_STEP / elapsed,
+        "finite_env_steps_per_sec": finite_total / elapsed,
+        "finite_note": "env-steps of envs whose kinematic state was finite at the start and at the end of the timed "
+                       "region (diverged envs carry NaN, as the reference's integrator does, and count in value)",
+        "estimated_ticks_per_sec": steps_total * MEAN_TICKS_PER_ENV_STEP / elapsed,
+        "estimated_ticks_note": "env-steps/s x 710.4, the oracle's mean ticks per env-step under random actions "
+                                "(not a measured tick count)",
         "budget_ticks_per_sec": budget_ticks / elapsed,
         "kernel_ms_per_launch": kern_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -392,6 +421,8 @@ def main(argv=None):
                 "source": prof[0],
                 "note": "PMC fp64 VALU instructions x 64 lanes (FMA = 2): both arms of branch-free selects, "
                         "Newton steps of divisions and polynomial transcendentals included"}
+    if parity is not None:
+        res["parity_sampled"] = parity
     if world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(a.cpu_baseline_seconds)
     print(json.dumps(res), flush=True)

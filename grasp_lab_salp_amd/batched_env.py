@@ -201,7 +201,8 @@ class BatchedSalpEnv:
         boundaries.  ``buffers``: dict of float32 [n_steps, n, ...] tensors
         obs, actions, rewards, episode_starts, values, log_probs (SB3's
         RolloutBuffer fields); ``episode_start`` [n] f32 in/out, ``last_obs``
-        [n, obs_dim] out, ``ep_stats`` [2] f64 and ``diverged`` [1] i64
+        [n, obs_dim] in/out (in: the observation each env's first step is
+        taken on, e.g. the one reset() returned), ``ep_stats`` [2] f64 and ``diverged`` [1] i64
         accumulated.  See include/salp.h for the exact semantics."""
         R = _lib.SalpPolicyRollout()
         w = weights

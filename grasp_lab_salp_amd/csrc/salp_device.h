@@ -132,6 +132,10 @@ SD double qdiv(double x, Rcp k) {
     const double q = sm_fma(sm_fma(-k.d, q0, x), k.r, q0);
     return __builtin_amdgcn_div_fixup(q, k.d, x);
 }
+/* One component a*b - c*d of np.cross (the reference multiplies, then
+ * subtracts), the product a*b fused into the difference in the SALP_FMA
+ * build (salp_math.h sm_mad; the oracle's cross() is the same expression). */
+SD double cross_c(double a, double b, double c, double d) { return sm_mad(a, b, -(c * d)); }
 SD float sqf(float x) { return (float)((double)x * (double)x); }
 SD float cubef(float x) {
     double p = (double)x * (double)x;
@@ -669,13 +673,13 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     /* ---------------- Newton ---------------- */
     /* Coriolis force -w x (M v)  (src/dynamics.py:159-162) */
     double mv0 = m * h.v0, mv1 = m * h.v1, mv2 = m * h.v2;
-    double cf0 = -(h.w1 * mv2 - h.w2 * mv1), cf1 = -(h.w2 * mv0 - h.w0 * mv2),
-           cf2 = -(h.w0 * mv1 - h.w1 * mv0);
+    double cf0 = -cross_c(h.w1, mv2, h.w2, mv1), cf1 = -cross_c(h.w2, mv0, h.w0, mv2),
+           cf2 = -cross_c(h.w0, mv1, h.w1, mv0);
     /* drag force (src/dynamics.py:110-116) */
     double vn = np_norm3(h.v0, h.v1, h.v2);
-    double df0 = g.kc0 * vn * h.v0 + g.kc0 * h.v0 * dfr;
-    double df1 = g.kc1 * vn * h.v1 + g.kc1 * h.v1 * dfr;
-    double df2 = g.kc1 * vn * h.v2 + g.kc1 * h.v2 * dfr;
+    double df0 = sm_mad(g.kc0 * h.v0, dfr, g.kc0 * vn * h.v0);
+    double df1 = sm_mad(g.kc1 * h.v1, dfr, g.kc1 * vn * h.v1);
+    double df2 = sm_mad(g.kc1 * h.v2, dfr, g.kc1 * vn * h.v2);
     /* jet force, JET phase only (src/robot.py:937-951, src/dynamics.py:87-101) */
     const bool jet = h.phase == JET;
     double jf0 = jet ? g.mr * (h.d0 * g.speed) * -cd : 0.0;
@@ -685,39 +689,38 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     double am0 = m * cam0, am1 = m * cam1, am2 = m * cam2;
     double amr0 = g.mr * car0, amr1 = g.mr * car1, amr2 = g.mr * car2;
     double amv0 = am0 * h.v0, amv1 = am1 * h.v1, amv2 = am2 * h.v2;
-    double af0 = -((am0 * h.a0 + (h.w1 * amv2 - h.w2 * amv1)) + amr0 * h.v0);
-    double af1 = -((am1 * h.a1 + (h.w2 * amv0 - h.w0 * amv2)) + amr1 * h.v1);
-    double af2 = -((am2 * h.a2 + (h.w0 * amv1 - h.w1 * amv0)) + amr2 * h.v2);
+    double af0 = -sm_mad(amr0, h.v0, sm_mad(am0, h.a0, cross_c(h.w1, amv2, h.w2, amv1)));
+    double af1 = -sm_mad(amr1, h.v1, sm_mad(am1, h.a1, cross_c(h.w2, amv0, h.w0, amv2)));
+    double af2 = -sm_mad(amr2, h.v2, sm_mad(am2, h.a2, cross_c(h.w0, amv1, h.w1, amv0)));
     /* fictitious forces of the moving center of mass (src/robot.py:806-810);
      * com = (cx, 0, 0) */
     const double cx = h.com, crx = h.comr;
     double acc_y = (h.w0 * (h.w1 * cx) + (h.w2 * crx) * 2.0) + h.al2 * cx;
     double acc_z = (h.w0 * (h.w2 * cx) + -(h.w1 * crx) * 2.0) + -(h.al1 * cx);
-    double acc_x = (h.w1 * -(h.w1 * cx) - h.w2 * (h.w2 * cx)) + h.coma;
-    double ff0 = acc_x * m, ff1 = acc_y * m, ff2 = acc_z * m;
+    double acc_x = cross_c(h.w1, -(h.w1 * cx), h.w2, h.w2 * cx) + h.coma;
     /* total force and linear acceleration (src/dynamics.py:5-10) */
     double na0, na1, na2;
     const Rcp rm{m, g.rm};
     if (RAND) {   /* + force noise (z: zero) */
-        na0 = qdiv(((((jf0 + df0) + af0) + cf0) + nf0) + ff0, rm);
-        na1 = qdiv(((((jf1 + df1) + af1) + cf1) + nf1) + ff1, rm);
-        na2 = qdiv(((((jf2 + df2) + af2) + cf2) + 0.0) + ff2, rm);
+        na0 = qdiv(sm_mad(acc_x, m, (((jf0 + df0) + af0) + cf0) + nf0), rm);
+        na1 = qdiv(sm_mad(acc_y, m, (((jf1 + df1) + af1) + cf1) + nf1), rm);
+        na2 = qdiv(sm_mad(acc_z, m, (((jf2 + df2) + af2) + cf2) + 0.0), rm);
     } else {
-        na0 = qdiv((((jf0 + df0) + af0) + cf0) + ff0, rm);
-        na1 = qdiv((((jf1 + df1) + af1) + cf1) + ff1, rm);
-        na2 = qdiv((((jf2 + df2) + af2) + cf2) + ff2, rm);
+        na0 = qdiv(sm_mad(acc_x, m, ((jf0 + df0) + af0) + cf0), rm);
+        na1 = qdiv(sm_mad(acc_y, m, ((jf1 + df1) + af1) + cf1), rm);
+        na2 = qdiv(sm_mad(acc_z, m, ((jf2 + df2) + af2) + cf2), rm);
     }
     /* ---------------- Euler ---------------- */
     const double I0 = g.I0, I1 = g.I1;
     /* Coriolis torque -w x (I w) (src/dynamics.py:165-168) */
     double iw0 = I0 * h.w0, iw1 = I1 * h.w1, iw2 = I1 * h.w2;
-    double ct0 = -(h.w1 * iw2 - h.w2 * iw1), ct1 = -(h.w2 * iw0 - h.w0 * iw2),
-           ct2 = -(h.w0 * iw1 - h.w1 * iw0);
+    double ct0 = -cross_c(h.w1, iw2, h.w2, iw1), ct1 = -cross_c(h.w2, iw0, h.w0, iw2),
+           ct2 = -cross_c(h.w0, iw1, h.w1, iw0);
     /* drag torque (src/dynamics.py:119-128) */
     double wn = np_norm3(h.w0, h.w1, h.w2);
-    double dt0 = g.ra0 * wn * h.w0 * g.dimx + g.ra0 * h.w0 * h.W * dtr;
-    double dt1 = g.ra1 * wn * h.w1 * g.dimy + g.ra1 * h.w1 * h.W * dtr;
-    double dt2 = g.ra1 * wn * h.w2 * g.dimy + g.ra1 * h.w2 * h.W * dtr;
+    double dt0 = sm_mad(g.ra0 * h.w0 * h.W, dtr, g.ra0 * wn * h.w0 * g.dimx);
+    double dt1 = sm_mad(g.ra1 * h.w1 * h.W, dtr, g.ra1 * wn * h.w1 * g.dimy);
+    double dt2 = sm_mad(g.ra1 * h.w2 * h.W, dtr, g.ra1 * wn * h.w2 * g.dimy);
     /* jet torque r x F, r = (mid_x - L/2, 0, 0) (src/robot.py:931-935) */
     double jt1 = -(g.rx * jf2), jt2 = g.rx * jf1;
     /* deformation torque -(dI/dt) w; prev_I <- I (src/robot.py:888-896) */
@@ -729,20 +732,20 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     /* added-mass torque, I_rate term identically zero (src/dynamics.py:144-156) */
     double at0 = I0 * cat0, at1 = I1 * cat1, at2 = I1 * cat2;
     double atw0 = at0 * h.w0, atw1 = at1 * h.w1, atw2 = at2 * h.w2;
-    double amt0 = -((at0 * h.al0 + (h.w1 * atw2 - h.w2 * atw1)) + (h.v1 * amv2 - h.v2 * amv1));
-    double amt1 = -((at1 * h.al1 + (h.w2 * atw0 - h.w0 * atw2)) + (h.v2 * amv0 - h.v0 * amv2));
-    double amt2 = -((at2 * h.al2 + (h.w0 * atw1 - h.w1 * atw0)) + (h.v0 * amv1 - h.v1 * amv0));
+    double amt0 = -(sm_mad(at0, h.al0, cross_c(h.w1, atw2, h.w2, atw1)) + cross_c(h.v1, amv2, h.v2, amv1));
+    double amt1 = -(sm_mad(at1, h.al1, cross_c(h.w2, atw0, h.w0, atw2)) + cross_c(h.v2, amv0, h.v0, amv2));
+    double amt2 = -(sm_mad(at2, h.al2, cross_c(h.w0, atw1, h.w1, atw0)) + cross_c(h.v0, amv1, h.v1, amv0));
     /* total torque and angular acceleration (src/dynamics.py:13-17) */
     double nal0, nal1, nal2;
     const Rcp rI0{I0, g.rI0}, rI1{I1, g.rI1};
     if (RAND) {   /* + torque noise (x, y: zero) */
-        nal0 = qdiv((((dt0 + ct0) + dft0) + amt0) + 0.0, rI0);
-        nal1 = qdiv(((((jt1 + dt1) + ct1) + dft1) + amt1) + 0.0, rI1);
-        nal2 = qdiv(((((jt2 + dt2) + ct2) + dft2) + amt2) + nt2, rI1);
+        nal0 = qdiv((sm_mad(-ir0, h.w0, dt0 + ct0) + amt0) + 0.0, rI0);
+        nal1 = qdiv((sm_mad(-ir1, h.w1, (jt1 + dt1) + ct1) + amt1) + 0.0, rI1);
+        nal2 = qdiv((sm_mad(-ir2, h.w2, (jt2 + dt2) + ct2) + amt2) + nt2, rI1);
     } else {
-        nal0 = qdiv(((dt0 + ct0) + dft0) + amt0, rI0);
-        nal1 = qdiv((((jt1 + dt1) + ct1) + dft1) + amt1, rI1);
-        nal2 = qdiv((((jt2 + dt2) + ct2) + dft2) + amt2, rI1);
+        nal0 = qdiv(sm_mad(-ir0, h.w0, dt0 + ct0) + amt0, rI0);
+        nal1 = qdiv(sm_mad(-ir1, h.w1, (jt1 + dt1) + ct1) + amt1, rI1);
+        nal2 = qdiv(sm_mad(-ir2, h.w2, (jt2 + dt2) + ct2) + amt2, rI1);
     }
     if (REC) {
         const double z = 0.0;
@@ -759,20 +762,20 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
         put(SALP_T_AMF0, af0); put(SALP_T_AMF1, af1); put(SALP_T_AMF2, af2);
         put(SALP_T_AMT0, amt0); put(SALP_T_AMT1, amt1); put(SALP_T_AMT2, amt2);
         put(SALP_T_DEFT0, dft0); put(SALP_T_DEFT1, dft1); put(SALP_T_DEFT2, dft2);
-        put(SALP_T_ACCF0, ff0); put(SALP_T_ACCF1, ff1); put(SALP_T_ACCF2, ff2);
+        put(SALP_T_ACCF0, acc_x * m); put(SALP_T_ACCF1, acc_y * m); put(SALP_T_ACCF2, acc_z * m);
     }
     h.a0 = na0; h.a1 = na1; h.a2 = na2;
     h.al0 = nal0; h.al1 = nal1; h.al2 = nal2;
     /* ---------------- integrate (semi-implicit Euler) ---------------- */
-    h.v0 = h.v0 + na0 * DT; h.v1 = h.v1 + na1 * DT; h.v2 = h.v2 + na2 * DT;
-    h.w0 = h.w0 + nal0 * DT; h.w1 = h.w1 + nal1 * DT; h.w2 = h.w2 + nal2 * DT;
+    h.v0 = sm_mad(na0, DT, h.v0); h.v1 = sm_mad(na1, DT, h.v1); h.v2 = sm_mad(na2, DT, h.v2);
+    h.w0 = sm_mad(nal0, DT, h.w0); h.w1 = sm_mad(nal1, DT, h.w1); h.w2 = sm_mad(nal2, DT, h.w2);
     {   /* to_euler_angle_rate_jit (src/dynamics.py:20-31) at the current angles */
         const Rcp rc = rcp_of(h.cth);
         double tt = qdiv(h.st, rc);
         double r0 = sm_fma(h.cp * tt, h.w2, h.w0 + (h.sp * tt) * h.w1);
         double r1 = sm_fma(-h.sp, h.w2, h.cp * h.w1);
         double r2 = sm_fma(qdiv(h.cp, rc), h.w2, qdiv(h.sp, rc) * h.w1);
-        h.e0 = h.e0 + r0 * DT; h.e1 = h.e1 + r1 * DT; h.e2 = h.e2 + r2 * DT;
+        h.e0 = sm_mad(r0, DT, h.e0); h.e1 = sm_mad(r1, DT, h.e1); h.e2 = sm_mad(r2, DT, h.e2);
         if (REC) {
             rec[(int64_t)SALP_T_ETAR0 * rs] = r0;
             rec[(int64_t)SALP_T_ETAR1 * rs] = r1;
@@ -787,10 +790,10 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
         Rot R = rot_sc(h.sp, h.cp, h.st, h.cth, ss, cs);
         double vw[3];
         rot_apply(R, h.v0, h.v1, h.v2, vw);
-        h.p0 = h.p0 + vw[0] * DT; h.p1 = h.p1 + vw[1] * DT; h.p2 = h.p2 + vw[2] * DT;
+        h.p0 = sm_mad(vw[0], DT, h.p0); h.p1 = sm_mad(vw[1], DT, h.p1); h.p2 = sm_mad(vw[2], DT, h.p2);
     }
-    h.q0 = h.q0 + h.v0 * DT; h.q1 = h.q1 + h.v1 * DT; h.q2 = h.q2 + h.v2 * DT;
-    h.g0 = h.g0 + h.w0 * DT; h.g1 = h.g1 + h.w1 * DT; h.g2 = h.g2 + h.w2 * DT;
+    h.q0 = sm_mad(h.v0, DT, h.q0); h.q1 = sm_mad(h.v1, DT, h.q1); h.q2 = sm_mad(h.v2, DT, h.q2);
+    h.g0 = sm_mad(h.w0, DT, h.g0); h.g1 = sm_mad(h.w1, DT, h.g1); h.g2 = sm_mad(h.w2, DT, h.g2);
     /* ---------------- clocks, phase, properties ---------------- */
     h.ct += DT;
     h.time += DT;

@@ -428,7 +428,14 @@ __device__ __forceinline__ void rollout_boundary(Hot& h, ST S, const Params& P, 
         }
         const bool beg = active && !pending;
         if (beg) {
-            if ((POL || B.obs_before) && !have_o) {
+            if (POL && !have_o) {
+                // first step of a salp_collect call: the observation the caller
+                // holds (last_obs is in/out: the previous call's last one, or the
+                // reset observation; with observation noise on, the noisy one the
+                // previous bootstrap value was computed from)
+                for (int k = 0; k < P.obs_dim; ++k) o[k] = R.last_obs[(size_t)i * P.obs_dim + k];
+                have_o = true;
+            } else if (B.obs_before && !have_o) {
                 // first step after create / reset / set_state / a previous call:
                 // the env's observation as reset() returns it (noise-free)
                 const salp::Rot Rt = salp::rot_zyx(h.e0, h.e1, h.e2);

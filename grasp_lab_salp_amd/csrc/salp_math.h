@@ -75,6 +75,26 @@ SM_QUAL int32_t sm_hi(double x) { return (int32_t)(sm_d2u(x) >> 32); }
 SM_QUAL double sm_fma(double a, double b, double c) { return fma(a, b, c); }
 SM_QUAL float sm_fmaf(float a, float b, float c) { return fmaf(a, b, c); }
 
+/* a * b + c at the points where the reference's NumPy expression is a
+ * product feeding a sum.  SALP_FMA = 1 (the default, device and oracle
+ * alike): fused, one rounding.  SALP_FMA = 0: NumPy's two roundings, the
+ * exact elementwise semantics of the reference (every other operation is the
+ * same in both modes).  The two modes differ by at most an ulp per such
+ * operation; tests/test_fma_mode.py measures how far that carries over whole
+ * episodes, tests/test_oracle_golden.py pins both against the reference.  The
+ * device and the oracle are always built in the same mode, so they agree bit
+ * for bit in either. */
+#ifndef SALP_FMA
+#define SALP_FMA 0
+#endif
+SM_QUAL double sm_mad(double a, double b, double c) {
+#if SALP_FMA
+    return fma(a, b, c);
+#else
+    return a * b + c;
+#endif
+}
+
 /* ------------------------------------------------ NumPy/OpenBLAS orders */
 /* np.linalg.norm of a 3-vector / 2-vector (ddot FMA chain, then sqrt). */
 SM_QUAL double np_norm3(double a, double b, double c) {
@@ -148,19 +168,30 @@ SM_QUAL SmPoly sm_poly(void) {
                 -2.75573143513906633035e-07, 2.08757232129817482790e-09,  -1.13596475577881948265e-11};
     return k;
 }
+/* fdlibm's kernels with the polynomial steps written as sm_mad: with
+ * SALP_FMA = 0 each line is fdlibm's expression exactly
+ * (r = S2 + z*(S3 + z*S4) + z*w*(S5 + z*S6), ...). */
+SM_QUAL double sm_ksin_r(double z, double w, SmPoly K) {
+    return sm_mad(z * w, sm_mad(z, K.S6, K.S5), sm_mad(z, sm_mad(z, K.S4, K.S3), K.S2));
+}
+/* x - ((z*(0.5*y - v*r) - y) - v*S1) */
+SM_QUAL double sm_ksin_tail(double x, double y, double z, double v, double r, SmPoly K) {
+    return x - sm_mad(-v, K.S1, sm_mad(z, sm_mad(-v, r, 0.5 * y), -y));
+}
 SM_QUAL double sm_ksin_p(double x, double y, int iy, SmPoly K) {
     double z = x * x, w = z * z;
-    double r = K.S2 + z * (K.S3 + z * K.S4) + z * w * (K.S5 + z * K.S6);
+    double r = sm_ksin_r(z, w, K);
     double v = z * x;
-    if (iy == 0) return x + v * (K.S1 + z * r);
-    return x - ((z * (0.5 * y - v * r) - y) - v * K.S1);
+    if (iy == 0) return sm_mad(v, sm_mad(z, r, K.S1), x);
+    return sm_ksin_tail(x, y, z, v, r, K);
 }
 SM_QUAL double sm_kcos_p(double x, double y, SmPoly K) {
     double z = x * x, w = z * z;
-    double r = z * (K.C1 + z * (K.C2 + z * K.C3)) + w * w * (K.C4 + z * (K.C5 + z * K.C6));
+    /* z*(C1 + z*(C2 + z*C3)) + w*w*(C4 + z*(C5 + z*C6)) */
+    double r = sm_mad(z, sm_mad(z, sm_mad(z, K.C3, K.C2), K.C1), (w * w) * sm_mad(z, sm_mad(z, K.C6, K.C5), K.C4));
     double hz = 0.5 * z;
     w = 1.0 - hz;
-    return w + (((1.0 - w) - hz) + (z * r - x * y));
+    return w + (((1.0 - w) - hz) + sm_mad(z, r, -(x * y)));
 }
 SM_QUAL double sm_ksin(double x, double y, int iy) { return sm_ksin_p(x, y, iy, sm_poly()); }
 SM_QUAL double sm_kcos(double x, double y) { return sm_kcos_p(x, y, sm_poly()); }
@@ -172,7 +203,7 @@ SM_QUAL int sm_rem_pio2(double x, double* y0, double* y1) {
                  pio2_2 = 6.07710050630396597660e-11, pio2_2t = 2.02226624879595063154e-21,
                  pio2_3 = 2.02226624871116645580e-21, pio2_3t = 8.47842766036889956997e-32;
     double fn = rint(x * invpio2);
-    double r = x - fn * pio2_1;
+    double r = sm_mad(-fn, pio2_1, x);   /* fn * pio2_1 is exact (33-bit pio2_1): same either way */
     double w = fn * pio2_1t;
     double y = r - w;
     int j = (sm_hi(x) >> 20) & 0x7ff;
@@ -236,9 +267,9 @@ SM_QUAL void sm_sincos_nb_p(double x, double* s_out, double* c_out, SmPoly K) {
     int n = sm_rem_pio2(x, &y0, &y1);
     if (small) { y0 = x; y1 = 0.0; n = 0; }
     const double z = y0 * y0, w = z * z;
-    const double r = K.S2 + z * (K.S3 + z * K.S4) + z * w * (K.S5 + z * K.S6);
+    const double r = sm_ksin_r(z, w, K);
     const double v = z * y0;
-    const double s = small ? y0 + v * (K.S1 + z * r) : y0 - ((z * (0.5 * y1 - v * r) - y1) - v * K.S1);
+    const double s = small ? sm_mad(v, sm_mad(z, r, K.S1), y0) : sm_ksin_tail(y0, y1, z, v, r, K);
     const double c = sm_kcos_p(y0, y1, K);
     const int q = n & 3;
     const double a = (q & 1) ? c : s, b = (q & 1) ? s : c;

@@ -472,6 +472,8 @@ class PPO:
         inside the simulation kernel (include/salp.h)."""
         b = self.buf
         w = pack_policy(self.policy, self._packed)
+        if self._obs is not self._last_obs:   # salp_collect takes the first observation from last_obs
+            self._last_obs.copy_(self._obs)
         guard = self.reset_nonfinite
         self.sim.collect(w, self.n_steps, {"obs": b.obs, "actions": b.actions, "rewards": b.rewards,
                                            "episode_starts": b.episode_starts, "values": b.values,
@@ -497,11 +499,17 @@ class PPO:
         :func:`diverged_mask` are reset on the spot and the step is recorded as
         a termination with reward 0 (no bootstrap from a diverged state).
         Sync-free: the masked reset is a no-op where the mask is all zero.
-        Returns (reward, diverged mask)."""
-        bad = diverged_mask(r.obs, rew)
+        The guard looks at the step's own observation: the terminal one where
+        the episode ended (r.obs is already the auto-reset observation there),
+        as salp_collect does; an env that ended its episode is not reset a
+        second time.  Returns (reward, diverged mask)."""
+        done = r.terminated | r.truncated
+        seen = torch.where(done.unsqueeze(1), r.terminal_obs, r.obs)
+        bad = diverged_mask(seen, rew)
         self._nonfinite = self._nonfinite + bad.sum()
-        fresh = self.sim.reset(mask=bad)
-        col = bad.unsqueeze(1)
+        again = bad & ~done
+        fresh = self.sim.reset(mask=again)
+        col = again.unsqueeze(1)
         r.obs.copy_(torch.where(col, fresh, r.obs))
         r.truncated |= bad
         r.terminated |= bad     # terminal: no gamma * V(terminal_obs) bootstrap

@@ -36,11 +36,14 @@ def reduce_run(elapsed_s, env_steps, kernel_ms, lockstep_rate, device=None):
 
 
 def reduce_sums(values, device=None):
-    """SUM of per-rank counters (e.g. diverged envs) over ranks; the inputs
-    themselves without an initialised process group.  Returns python ints."""
-    vals = [int(v) for v in values]
+    """SUM of per-rank counters (e.g. diverged envs) or rates over ranks; the
+    inputs themselves without an initialised process group.  Python ints stay
+    ints (summed exactly as int64), anything else is summed as float64."""
+    ints = [isinstance(v, int) and not isinstance(v, bool) for v in values]
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
-        return vals
-    t = torch.tensor(vals, dtype=torch.int64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return [int(x) for x in t.tolist()]
+        return [int(v) if k else float(v) for v, k in zip(values, ints)]
+    ti = torch.tensor([int(v) if k else 0 for v, k in zip(values, ints)], dtype=torch.int64, device=device)
+    tf = torch.tensor([0.0 if k else float(v) for v, k in zip(values, ints)], dtype=torch.float64, device=device)
+    dist.all_reduce(ti, op=dist.ReduceOp.SUM)
+    dist.all_reduce(tf, op=dist.ReduceOp.SUM)
+    return [int(a) if k else float(b) for a, b, k in zip(ti.tolist(), tf.tolist(), ints)]

@@ -267,6 +267,8 @@ class SalpVecEnv(_VecEnvBase):
 # SB3's in-process / subprocess VecEnv classes: for the batched simulator both
 # mean "all envs in one kernel launch", which is what SalpVecEnv is.
 _BATCHED_EQUIVALENT = ("DummyVecEnv", "SubprocVecEnv")
+# SalpVecEnv constructor options a caller may pass through vec_env_kwargs
+_BATCHED_KWARGS = frozenset({"device", "infos"})
 
 
 def make_vec_env(env_id, n_envs=1, seed=None, start_index=0, monitor_dir=None, wrapper_class=None,
@@ -300,12 +302,22 @@ def make_vec_env(env_id, n_envs=1, seed=None, start_index=0, monitor_dir=None, w
         finally:
             env.close()
         cls = vec_env_cls if (isinstance(vec_env_cls, type) and issubclass(vec_env_cls, SalpVecEnv)) else SalpVecEnv
-        return cls(n_envs, params=params, seed=0 if seed is None else seed, env_id_offset=start_index,
-                   **(vec_env_kwargs or {}) if cls is not SalpVecEnv else {})
+        kw = dict(vec_env_kwargs or {})
+        # SubprocVecEnv's process options have no meaning for one batched launch
+        kw.pop("start_method", None)
+        unknown = sorted(set(kw) - _BATCHED_KWARGS) if cls is SalpVecEnv else []
+        if unknown:
+            raise TypeError(f"make_vec_env: vec_env_kwargs {unknown} do not apply to the batched SalpVecEnv "
+                            f"(accepted: {sorted(_BATCHED_KWARGS | {'start_method'})})")
+        return cls(n_envs, params=params, seed=0 if seed is None else seed, env_id_offset=start_index, **kw)
 
     def make(rank):
         def _init():
             e = env_id(**env_kwargs)
+            if seed is not None and hasattr(e, "action_space"):
+                # SB3 seeds each env's action space with seed + rank (the env
+                # itself is seeded at its next reset through VecEnv.seed)
+                e.action_space.seed(seed + rank)
             if wrapper_class is not None:
                 e = wrapper_class(e, **(wrapper_kwargs or {}))
             return e
@@ -314,4 +326,7 @@ def make_vec_env(env_id, n_envs=1, seed=None, start_index=0, monitor_dir=None, w
     if vec_env_cls is None or cls_name in _BATCHED_EQUIVALENT:
         if cls_name is None:
             raise ValueError("wrapper_class needs a per-env vec_env_cls (e.g. SB3's DummyVecEnv)")
-    return vec_env_cls(fns, **(vec_env_kwargs or {}))
+    venv = vec_env_cls(fns, **(vec_env_kwargs or {}))
+    if seed is not None and hasattr(venv, "seed"):
+        venv.seed(seed)   # SB3: env i is seeded with seed + i at its next reset
+    return venv

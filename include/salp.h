@@ -189,11 +189,12 @@ int salp_step_random(SalpEnv* h, int32_t n_steps, double* reward_sum_out, void* 
  *                  0 and a fresh episode where the divergence guard fires
  *                  (|obs| > diverged_obs_abs, |reward| > diverged_reward_abs or
  *                  non-finite; guard off when diverged_obs_abs <= 0);
- * then episode_start[i] (next step starts an episode) and last_obs[i] (the obs
- * after the last step, the reset obs where it ended an episode).
+ * last_obs[i] is in/out: on entry the observation env i's first step of this
+ * call is taken on (the reset observation, or the previous call's last_obs);
+ * on return episode_start[i] (next step starts an episode) and last_obs[i]
+ * (the obs after the last step, the reset obs where it ended an episode).
  * ep_stats[0..1] += (return, 1) per episode that ended by the task's rules;
- * diverged[0] += envs reset by the guard.  With observation noise on, the
- * observation at the first step of a call is the noise-free one. */
+ * diverged[0] += envs reset by the guard. */
 typedef struct SalpPolicyRollout {
     const float* weights;  /* [SALP_POLICY_SIZE] */
     uint64_t noise_seed;
@@ -208,7 +209,7 @@ typedef struct SalpPolicyRollout {
     float* values;         /* [n_steps][n_envs]           */
     float* log_probs;      /* [n_steps][n_envs]           */
     float* episode_start;  /* [n_envs] in/out             */
-    float* last_obs;       /* [n_envs][obs_dim] out       */
+    float* last_obs;       /* [n_envs][obs_dim] in/out    */
     double* ep_stats;      /* [2] accumulated             */
     int64_t* diverged;     /* [1] accumulated             */
 } SalpPolicyRollout;

@@ -15,8 +15,11 @@ from grasp_lab_salp_amd._abi import (INFO_DIM, MAX_OBSTACLES, NUM_FIELDS, OBS_DI
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libsalp_oracle.so")
+# the same restatement with NumPy's unfused product-sums (SALP_FMA=0,
+# salp_math.h); libsalp.so and LIB_PATH are built with SALP_FMA=1
+EXACT_LIB_PATH = os.path.join(HERE, "libsalp_oracle_exact.so")
 
-_lib = None
+_libs = {}
 
 
 SOURCES = [os.path.join(HERE, "salp_oracle.c"), os.path.join(HERE, "..", "include", "salp.h")] + [
@@ -25,18 +28,19 @@ SOURCES = [os.path.join(HERE, "salp_oracle.c"), os.path.join(HERE, "..", "includ
 
 
 def build(force=False):
-    stale = not os.path.exists(LIB_PATH) or any(
-        os.path.getmtime(s) > os.path.getmtime(LIB_PATH) for s in SOURCES)
+    stale = any(not os.path.exists(p) or any(os.path.getmtime(s) > os.path.getmtime(p) for s in SOURCES)
+                for p in (LIB_PATH, EXACT_LIB_PATH))
     if force or stale:
         subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB_PATH
 
 
-def lib():
-    global _lib
-    if _lib is None:
+def lib(exact=False):
+    """The oracle library: the product's arithmetic mode, or (exact) NumPy's
+    unfused products and sums."""
+    if exact not in _libs:
         build()
-        L = ctypes.CDLL(LIB_PATH)
+        L = ctypes.CDLL(EXACT_LIB_PATH if exact else LIB_PATH)
         P = ctypes.POINTER
         d, f, u8, i32, i64, u32 = (ctypes.c_double, ctypes.c_float, ctypes.c_uint8,
                                    ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32)
@@ -50,6 +54,9 @@ def lib():
         L.oracle_step_random.argtypes = [sp, i64, P(d), i32, ctypes.c_uint64, i64, P(d),
                                          ctypes.c_int]
         L.oracle_step_random.restype = i64
+        L.oracle_replay.argtypes = [sp, i64, P(i64), P(i64), P(d), ctypes.c_uint64, P(d), i64, P(f), P(f),
+                                    P(f), P(f), P(u8), ctypes.c_int, ctypes.c_int]
+        L.oracle_replay.restype = i64
         L.oracle_robot_trace.argtypes = [sp, P(f), ctypes.c_int, P(d), i64]
         L.oracle_robot_trace.restype = i64
         L.oracle_math_selftest.argtypes = [P(d), P(d), i64, P(d)]
@@ -61,8 +68,8 @@ def lib():
         L.oracle_philox.argtypes = [u32] * 6 + [P(u32)]
         if L.oracle_num_fields() != NUM_FIELDS:
             raise RuntimeError("oracle / _abi field count mismatch")
-        _lib = L
-    return _lib
+        _libs[exact] = L
+    return _libs[exact]
 
 
 def _p(a, ct):
@@ -72,14 +79,15 @@ def _p(a, ct):
 class Oracle:
     """Batch of reference-equivalent envs on the CPU; state is [NUM_FIELDS, n]."""
 
-    def __init__(self, params=None, n_envs=1, seed=0, env_offset=0):
+    def __init__(self, params=None, n_envs=1, seed=0, env_offset=0, exact=False):
+        self._L = lib(exact)
         self.params = params if params is not None else default_params()
         self.n = int(n_envs)
         self.seed = int(seed)
         self.env_offset = int(env_offset)
         self.obs_dim = 6 + 2 * self.params.num_obstacles
         self.state = np.zeros((NUM_FIELDS, self.n), np.float64)
-        lib().oracle_init(ctypes.byref(self.params), self.n, _p(self.state, ctypes.c_double))
+        self._L.oracle_init(ctypes.byref(self.params), self.n, _p(self.state, ctypes.c_double))
 
     def _mask(self, mask):
         if mask is None:
@@ -89,7 +97,7 @@ class Oracle:
     def reset(self, mask=None):
         obs = np.zeros((self.n, self.obs_dim), np.float32)
         m = self._mask(mask)
-        lib().oracle_reset(ctypes.byref(self.params), self.n, _p(self.state, ctypes.c_double),
+        self._L.oracle_reset(ctypes.byref(self.params), self.n, _p(self.state, ctypes.c_double),
                            _p(m, ctypes.c_uint8), self.seed, self.env_offset,
                            _p(obs, ctypes.c_float), self.obs_dim)
         return obs
@@ -102,7 +110,7 @@ class Oracle:
         k = np.ascontiguousarray(n_obstacles, np.int32).reshape(self.n)
         obs = np.zeros((self.n, self.obs_dim), np.float32)
         m = self._mask(mask)
-        lib().oracle_reset_to(ctypes.byref(self.params), self.n, _p(self.state, ctypes.c_double),
+        self._L.oracle_reset_to(ctypes.byref(self.params), self.n, _p(self.state, ctypes.c_double),
                               _p(m, ctypes.c_uint8), _p(t, ctypes.c_float), _p(o, ctypes.c_float),
                               _p(k, ctypes.c_int32), _p(obs, ctypes.c_float), self.obs_dim)
         return obs
@@ -115,7 +123,7 @@ class Oracle:
                    terminal_obs=np.zeros((self.n, self.obs_dim), np.float32),
                    info=np.zeros((self.n, INFO_DIM), np.float64),
                    ticks=np.zeros(self.n, np.int64))
-        lib().oracle_step(ctypes.byref(self.params), self.n, _p(self.state, ctypes.c_double),
+        self._L.oracle_step(ctypes.byref(self.params), self.n, _p(self.state, ctypes.c_double),
                           _p(a, ctypes.c_float), _p(out["obs"], ctypes.c_float),
                           _p(out["reward"], ctypes.c_double), _p(out["terminated"], ctypes.c_uint8),
                           _p(out["truncated"], ctypes.c_uint8), int(bool(auto_reset)),
@@ -126,22 +134,22 @@ class Oracle:
 
     # ---- Robot / Nozzle level (salp_robot_*, salp_nozzle_* of include/salp.h)
     def robot_reset(self, mask=None):
-        lib().oracle_robot_reset(ctypes.byref(self.params), self.n, _p(self.state, ctypes.c_double),
+        self._L.oracle_robot_reset(ctypes.byref(self.params), self.n, _p(self.state, ctypes.c_double),
                                  _p(self._mask(mask), ctypes.c_uint8))
 
     def nozzle_set_angles(self, angles):
         a = np.ascontiguousarray(angles, np.float64).reshape(self.n, 2)
-        lib().oracle_nozzle_set_angles(ctypes.byref(self.params), self.n,
+        self._L.oracle_nozzle_set_angles(ctypes.byref(self.params), self.n,
                                        _p(self.state, ctypes.c_double), _p(a, ctypes.c_double))
 
     def nozzle_solve(self, yaw, yaw_f32):
         y = np.ascontiguousarray(yaw, np.float64).reshape(self.n)
-        lib().oracle_nozzle_solve(ctypes.byref(self.params), self.n, _p(self.state, ctypes.c_double),
+        self._L.oracle_nozzle_solve(ctypes.byref(self.params), self.n, _p(self.state, ctypes.c_double),
                                   _p(y, ctypes.c_double), int(bool(yaw_f32)))
 
     def robot_set_control(self, control, contraction_f32):
         c = np.ascontiguousarray(control, np.float64).reshape(self.n, 4)
-        lib().oracle_robot_set_control(ctypes.byref(self.params), self.n,
+        self._L.oracle_robot_set_control(ctypes.byref(self.params), self.n,
                                        _p(self.state, ctypes.c_double), _p(c, ctypes.c_double),
                                        int(bool(contraction_f32)), self.seed, self.env_offset)
 
@@ -153,7 +161,7 @@ class Oracle:
         if max_samples > 0:
             rows = np.full((max_samples, TRACE_DIM, self.n), np.nan)
             ns = np.zeros(self.n, np.int64)
-        lib().oracle_robot_cycle(ctypes.byref(self.params), self.n, _p(self.state, ctypes.c_double),
+        self._L.oracle_robot_cycle(ctypes.byref(self.params), self.n, _p(self.state, ctypes.c_double),
                                  _p(rows, ctypes.c_double), int(max_samples),
                                  _p(ns, ctypes.c_int64), _p(ticks, ctypes.c_int64), self.seed,
                                  self.env_offset)
@@ -185,28 +193,55 @@ class Oracle:
 
     def step_random(self, n_steps, threads=0):
         rs = np.zeros(self.n, np.float64)
-        ticks = lib().oracle_step_random(ctypes.byref(self.params), self.n,
+        ticks = self._L.oracle_step_random(ctypes.byref(self.params), self.n,
                                          _p(self.state, ctypes.c_double), int(n_steps), self.seed,
                                          self.env_offset, _p(rs, ctypes.c_double), int(threads))
         return rs, int(ticks)
 
 
-def robot_trace(actions, params=None, max_rows=200000):
+def replay(env_ids, n_steps, ct_stop=None, seed=0, params=None, capacity=0, threads=0, exact=False):
+    """Sampled envs of a chained random-action rollout (oracle_replay): env j,
+    global id env_ids[j], from creation through n_steps[j] env-steps, then the
+    in-flight cycle up to cycle_time ct_stop[j] (< 0: none).  Returns (state
+    [NUM_FIELDS, n], buffers {obs, obs_before, actions, rewards, dones} with
+    `capacity` slots (slot = step % capacity, the last `capacity` steps)."""
+    params = params if params is not None else default_params()
+    ids = np.ascontiguousarray(env_ids, np.int64)
+    n = len(ids)
+    ks = np.ascontiguousarray(n_steps, np.int64).reshape(n)
+    ct = None if ct_stop is None else np.ascontiguousarray(ct_stop, np.float64).reshape(n)
+    od = 6 + 2 * params.num_obstacles
+    state = np.zeros((NUM_FIELDS, n), np.float64)
+    cap = int(capacity)
+    b = {"obs": np.full((max(cap, 1), n, od), np.nan, np.float32),
+         "obs_before": np.full((max(cap, 1), n, od), np.nan, np.float32),
+         "actions": np.full((max(cap, 1), n, 3), np.nan, np.float32),
+         "rewards": np.full((max(cap, 1), n), np.nan, np.float32),
+         "dones": np.full((max(cap, 1), n), 255, np.uint8)}
+    lib(exact).oracle_replay(ctypes.byref(params), n, _p(ids, ctypes.c_int64), _p(ks, ctypes.c_int64),
+                        _p(ct, ctypes.c_double), int(seed), _p(state, ctypes.c_double), cap,
+                        _p(b["obs"], ctypes.c_float), _p(b["obs_before"], ctypes.c_float),
+                        _p(b["actions"], ctypes.c_float), _p(b["rewards"], ctypes.c_float),
+                        _p(b["dones"], ctypes.c_uint8), od, int(threads))
+    return state, (b if cap > 0 else None)
+
+
+def robot_trace(actions, params=None, max_rows=200000, exact=False):
     params = params if params is not None else default_params()
     a = np.ascontiguousarray(actions, np.float32).reshape(-1, 3)
     out = np.zeros((max_rows, 29), np.float64)
-    n = lib().oracle_robot_trace(ctypes.byref(params), _p(a, ctypes.c_float), len(a),
+    n = lib(exact).oracle_robot_trace(ctypes.byref(params), _p(a, ctypes.c_float), len(a),
                                  _p(out, ctypes.c_double), max_rows)
     if n < 0:
         raise RuntimeError("trace buffer too small")
     return out[:n]
 
 
-def math_selftest(x, y):
+def math_selftest(x, y, exact=False):
     x = np.ascontiguousarray(x, np.float64)
     y = np.ascontiguousarray(y, np.float64)
     out = np.zeros((12, len(x)), np.float64)
-    lib().oracle_math_selftest(_p(x, ctypes.c_double), _p(y, ctypes.c_double), len(x),
+    lib(exact).oracle_math_selftest(_p(x, ctypes.c_double), _p(y, ctypes.c_double), len(x),
                                _p(out, ctypes.c_double))
     return out
 

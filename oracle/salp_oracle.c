@@ -77,10 +77,19 @@ static V3 mTvec(M3 a, V3 x) {
         r.v[i] = np_dot_fwd(a.m[0][i], a.m[1][i], a.m[2][i], x.v[0], x.v[1], x.v[2]);
     return r;
 }
-/* np.cross: multiply then subtract, per component */
+/* np.cross: multiply then subtract, per component (the first product fused
+ * into the difference in the SALP_FMA build, salp_math.h sm_mad) */
 static V3 cross(V3 a, V3 b) {
-    return v3(a.v[1] * b.v[2] - a.v[2] * b.v[1], a.v[2] * b.v[0] - a.v[0] * b.v[2],
-              a.v[0] * b.v[1] - a.v[1] * b.v[0]);
+    return v3(sm_mad(a.v[1], b.v[2], -(a.v[2] * b.v[1])), sm_mad(a.v[2], b.v[0], -(a.v[0] * b.v[2])),
+              sm_mad(a.v[0], b.v[1], -(a.v[1] * b.v[0])));
+}
+/* a * s + b per component (b + a * s of the reference, fused with SALP_FMA) */
+static V3 vmad(V3 a, double s, V3 b) {
+    return v3(sm_mad(a.v[0], s, b.v[0]), sm_mad(a.v[1], s, b.v[1]), sm_mad(a.v[2], s, b.v[2]));
+}
+/* a * b + c per component */
+static V3 vmadv(V3 a, V3 b, V3 c) {
+    return v3(sm_mad(a.v[0], b.v[0], c.v[0]), sm_mad(a.v[1], b.v[1], c.v[1]), sm_mad(a.v[2], b.v[2], c.v[2]));
 }
 static double norm3(V3 a) { return np_norm3(a.v[0], a.v[1], a.v[2]); }
 static double pymax(double a, double b) { return b > a ? b : a; } /* Python max(a, b) */
@@ -505,7 +514,7 @@ static V3 compute_drag_force(double density, V3 area, V3 cd, V3 vel, double rati
         for (int i = 0; i < 3; ++i) ka.v[i] = (double)((float)k * (float)area.v[i]);
     V3 fq = vmul(vmuls(vmul(ka, cd), vn), vel);
     V3 fl = vmul(vmul(ka, cd), vel);
-    return vadd(fq, vmuls(fl, ratio));
+    return vmad(fl, ratio, fq);   /* fq + fl * ratio */
 }
 /* src/dynamics.py:119-128 */
 static V3 compute_drag_torque(double density, V3 rcd, V3 area, V3 w, double width, double length,
@@ -516,21 +525,35 @@ static V3 compute_drag_torque(double density, V3 rcd, V3 area, V3 w, double widt
     double k = -0.5 * density;
     V3 tq = vmul(vmul(vmuls(vmul(vmuls(rcd, k), area), wn), w), dims);
     V3 tl = vmuls(vmul(vmul(vmuls(rcd, k), area), w), width);
-    return vadd(tq, vmuls(tl, ratio));
+    return vmad(tl, ratio, tq);   /* tq + tl * ratio */
 }
 /* src/dynamics.py:131-141 */
 static V3 compute_added_mass_force(M3 mass, M3 amc, M3 mass_rate, M3 amrc, V3 acc, V3 w, V3 vel) {
     M3 am = mmul(mass, amc), amr = mmul(mass_rate, amrc);
+#if SALP_FMA
+    /* am and amr are products of diagonal matrices (exactly diagonal), so
+     * t1 = am @ acc and t3 = amr @ vel are diag * vector, fused into the sums */
+    V3 t2 = cross(w, mvec(am, vel));
+    return vneg(vmadv(v3(amr.m[0][0], amr.m[1][1], amr.m[2][2]), vel,
+                      vmadv(v3(am.m[0][0], am.m[1][1], am.m[2][2]), acc, t2)));
+#else
     V3 t1 = mvec(am, acc), t2 = cross(w, mvec(am, vel)), t3 = mvec(amr, vel);
     return vneg(vadd(vadd(t1, t2), t3));
+#endif
 }
 /* src/dynamics.py:144-156 */
 static V3 compute_added_mass_torque(M3 I, M3 amct, M3 I_rate, M3 amrct, M3 mass, M3 amcf,
                                     V3 alpha, V3 w, V3 vel) {
     M3 am = mmul(I, amct), amr = mmul(I_rate, amrct), afm = mmul(mass, amcf);
-    V3 t1 = mvec(am, alpha), t2 = cross(w, mvec(am, w)), t3 = mvec(amr, w);
+    V3 t2 = cross(w, mvec(am, w)), t3 = mvec(amr, w);
     V3 t4 = cross(vel, mvec(afm, vel));
-    return vneg(vadd(vadd(vadd(t1, t2), t3), t4));
+#if SALP_FMA
+    /* am diagonal (I and amct are): t1 = am @ alpha fused into t1 + t2 */
+    V3 t12 = vmadv(v3(am.m[0][0], am.m[1][1], am.m[2][2]), alpha, t2);
+#else
+    V3 t12 = vadd(mvec(am, alpha), t2);
+#endif
+    return vneg(vadd(vadd(t12, t3), t4));
 }
 /* src/dynamics.py:20-31 */
 static V3 to_euler_angle_rate(V3 eta, V3 w) {
@@ -729,9 +752,12 @@ static V3 robot_newton(Obj* o) {
     V3 a_cen = cross(o->w, cross(o->w, o->com));
     V3 a_cor = vmuls(cross(o->w, o->com_rate), 2.0);
     V3 a_rec = o->com_acc;
-    o->acceleration_force = vmuls(vadd(vadd(vadd(a_cen, a_cor), a_tan), a_rec), o->mass.m[0][0]);
-    V3 total = vadd(vadd(vadd(vadd(vadd(o->jet_force, o->drag_force), o->added_mass_force),
-                              o->coriolis_force), noise), o->acceleration_force);
+    V3 a_sum = vadd(vadd(vadd(a_cen, a_cor), a_tan), a_rec);
+    o->acceleration_force = vmuls(a_sum, o->mass.m[0][0]);
+    /* + acceleration_force, the product fused with SALP_FMA */
+    V3 total = vmad(a_sum, o->mass.m[0][0],
+                    vadd(vadd(vadd(vadd(o->jet_force, o->drag_force), o->added_mass_force), o->coriolis_force),
+                         noise));
     /* np.linalg.solve(diag(m), F) == F / m (probed) */
     return v3(total.v[0] / o->mass.m[0][0], total.v[1] / o->mass.m[1][1], total.v[2] / o->mass.m[2][2]);
 }
@@ -742,28 +768,35 @@ static V3 robot_euler(Obj* o) {
     o->drag_torque = compute_drag_torque(o->density, o->rcd, o->area, o->w, o->width, o->length,
                                          o->drag_torque_ratio, o->g32);
     o->jet_torque = cross(r_jet_moment_arm(o), o->jet_force);
-    o->deform_torque = vneg(mvec(r_get_inertia_rate(o), o->w));
+    const M3 Ir_w = r_get_inertia_rate(o);
+    o->deform_torque = vneg(mvec(Ir_w, o->w));
     M3 I_a = r_get_inertia(o);
     M3 Ir_a = r_get_inertia_rate(o); /* prev_I was just updated: exactly zero */
     o->added_mass_torque = compute_added_mass_torque(I_a, o->amt, Ir_a, o->amrt, r_get_mass(o),
                                                      o->amf, o->alpha, o->w, o->v);
     V3 noise = o->rand_dist ? o->ou_torque : vzero();
     M3 I = r_get_inertia(o);
-    V3 total = vadd(vadd(vadd(vadd(vadd(vadd(o->jet_torque, o->drag_torque), o->coriolis_torque),
-                                        o->asymmetry_torque), o->deform_torque),
-                         o->added_mass_torque), noise);
+    V3 part = vadd(vadd(vadd(o->jet_torque, o->drag_torque), o->coriolis_torque), o->asymmetry_torque);
+#if SALP_FMA
+    /* + deform_torque = -(I_rate @ w), I_rate diagonal: fused into the sum */
+    part = vmadv(v3(-Ir_w.m[0][0], -Ir_w.m[1][1], -Ir_w.m[2][2]), o->w, part);
+#else
+    part = vadd(part, o->deform_torque);
+#endif
+    V3 total = vadd(vadd(part, o->added_mass_torque), noise);
     return v3(total.v[0] / I.m[0][0], total.v[1] / I.m[1][1], total.v[2] / I.m[2][2]);
 }
 /* src/robot.py:860-875 */
 static void robot_update_motion_states(Obj* o) {
-    o->v = vadd(o->v, vmuls(o->acc, DT));
-    o->w = vadd(o->w, vmuls(o->alpha, DT));
+    /* x + rate * dt: fused with SALP_FMA */
+    o->v = vmad(o->acc, DT, o->v);
+    o->w = vmad(o->alpha, DT, o->w);
     o->eta_rate = to_euler_angle_rate(o->eta, o->w);
-    o->eta = vadd(o->eta, vmuls(o->eta_rate, DT));
+    o->eta = vmad(o->eta_rate, DT, o->eta);
     o->vw = to_world_frame(o->eta, o->v);
-    o->pw = vadd(o->pw, vmuls(o->vw, DT));
-    o->pos = vadd(o->pos, vmuls(o->v, DT));
-    o->ang = vadd(o->ang, vmuls(o->w, DT));
+    o->pw = vmad(o->vw, DT, o->pw);
+    o->pos = vmad(o->v, DT, o->pos);
+    o->ang = vmad(o->w, DT, o->ang);
 }
 /* src/robot.py:670-678, 854-858 */
 static void robot_step(Obj* o) {
@@ -817,13 +850,19 @@ static void robot_record(Obj* o, double* rec, int64_t rs, int first) {
 
 /* src/robot.py:740-777; returns the tick count.  rows != NULL: record
  * (record=True), sample t of this env at rows + t * SALP_TRACE_DIM * rs. */
-static int64_t robot_step_through_cycle(Obj* o, double* rows, int64_t rs, int64_t max_samples,
-                                        int64_t* n_samples) {
+/* The loop's prologue (src/robot.py:740-748): the previous cycle's
+ * displacement over this cycle's total time.  Returns the total. */
+static double robot_cycle_prologue(Obj* o) {
     double total = pymax(o->refill_time, o->nz.turn_time) + o->jet_time + o->coast_time;
     o->avg_v = vdivs(vsub(o->pos, o->ppos), total);
     o->avg_w = vdivs(vsub(o->ang, o->pang), total);
     o->ppos = o->pos;
     o->pang = o->ang;
+    return total;
+}
+static int64_t robot_step_through_cycle(Obj* o, double* rows, int64_t rs, int64_t max_samples,
+                                        int64_t* n_samples) {
+    const double total = robot_cycle_prologue(o);
     if (rows && max_samples > 0) robot_record(o, rows, rs, 1);
     int64_t n = 0;
     while (o->cycle_time < total) {
@@ -928,8 +967,8 @@ static void env_rescale_action(const float* a, float* r) {
     r[2] = a[2] * (float)(PI / 2);
 }
 
-/* src/salp_robot_env.py:196-210 (first half of step: through the cycle) */
-static int64_t env_begin_and_run_cycle(Obj* o, const float* action) {
+/* src/salp_robot_env.py:196-209 (step up to step_through_cycle) */
+static void env_begin(Obj* o, const float* action) {
     o->action[0] = action[0]; o->action[1] = action[1]; o->action[2] = action[2];
     float r[3];
     env_rescale_action(action, r);
@@ -944,6 +983,10 @@ static int64_t env_begin_and_run_cycle(Obj* o, const float* action) {
         nozzle_solve_angles(&o->nz, 1);
         robot_set_control(o, (double)r[0], (double)r[1], o->nz.angle1, o->nz.angle2, 1);
     }
+}
+/* src/salp_robot_env.py:196-210 (first half of step: through the cycle) */
+static int64_t env_begin_and_run_cycle(Obj* o, const float* action) {
+    env_begin(o, action);
     return robot_step_through_cycle(o, NULL, 0, 0, NULL);
 }
 
@@ -1349,6 +1392,82 @@ int64_t oracle_step_random(const SalpParams* p, int64_t n, double* state, int32_
         }
         if (reward_sum) reward_sum[i] = rs;
         obj_pack(&o, state, n, i);
+    }
+    return total_ticks;
+}
+
+/* Replay of sampled envs of a chained random-action rollout (the bench
+ * workload, salp_rollout): env j, global id env_ids[j], is constructed and
+ * reset as salp_create does, then runs n_steps[j] env-steps with Philox
+ * actions and auto-reset; if ct_stop[j] >= 0 it then begins its next env-step
+ * and ticks that cycle while cycle_time < ct_stop[j] (the in-flight cycle a
+ * launch leaves pending: the device state's cycle_time).  The rollout-buffer
+ * rows of the last `cap` env-steps go to slot (k % cap) of obs / obs_before
+ * [cap][n][obs_dim], actions [cap][n][3], rewards [cap][n] (float32) and
+ * dones [cap][n] (terminated | truncated << 1), as k_rollout writes them;
+ * the in-flight env-step's obs_before goes to its slot too.
+ * state: [NUM_FIELDS][n].  Returns the total ticks. */
+int64_t oracle_replay(const SalpParams* p, int64_t n, const int64_t* env_ids, const int64_t* n_steps,
+                      const double* ct_stop, uint64_t seed, double* state, int64_t cap, float* obs,
+                      float* obs_before, float* actions, float* rewards, uint8_t* dones, int obs_dim,
+                      int nthreads) {
+    int64_t total_ticks = 0;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#else
+    (void)nthreads;
+#endif
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : total_ticks)
+    for (int64_t j = 0; j < n; ++j) {
+        /* constructor, then reset (salp_create: k_construct + k_reset) */
+        double s1[SALP_NUM_FIELDS];
+        Obj o;
+        robot_init(&o, p);
+        o.n_obst = 0;
+        obj_pack(&o, s1, 1, 0);
+        obj_unpack(&o, p, s1, 1, 0, seed, env_ids[j]);
+        const uint64_t id = (uint64_t)env_ids[j];
+        float cur[SALP_OBS_DIM_MAX], tgt[2], obst[2 * SALP_MAX_OBSTACLES];
+        int nob;
+        env_draw_reset(&o, seed, id, tgt, obst, &nob);
+        env_reset_with(&o, tgt, obst, nob, cur);
+        for (int64_t k = 0; k < n_steps[j]; ++k) {
+            float a[3], ob[SALP_OBS_DIM_MAX];
+            uint8_t te, tr;
+            sp_action(seed, id, (uint64_t)o.step_count, a);
+            const int rec = cap > 0 && k >= n_steps[j] - cap;
+            const size_t row = (size_t)(k % (cap > 0 ? cap : 1)) * (size_t)n + (size_t)j;
+            if (rec && obs_before) memcpy(obs_before + row * obs_dim, cur, sizeof(float) * obs_dim);
+            total_ticks += env_begin_and_run_cycle(&o, a);
+            o.step_count += 1.0;
+            double rw = env_finish_step(&o, ob, &te, &tr, NULL);
+            if (rec) {
+                if (obs) memcpy(obs + row * obs_dim, ob, sizeof(float) * obs_dim);
+                if (actions) memcpy(actions + row * 3, a, sizeof(float) * 3);
+                if (rewards) rewards[row] = (float)rw;
+                if (dones) dones[row] = (uint8_t)(te | (tr << 1));
+            }
+            if (te || tr) {
+                env_draw_reset(&o, seed, id, tgt, obst, &nob);
+                env_reset_with(&o, tgt, obst, nob, ob);
+            }
+            memcpy(cur, ob, sizeof(float) * obs_dim);
+        }
+        if (ct_stop && ct_stop[j] >= 0.0) {
+            float a[3];
+            sp_action(seed, id, (uint64_t)o.step_count, a);
+            if (cap > 0 && obs_before)   /* the in-flight step's row: only its obs_before is written */
+                memcpy(obs_before + ((size_t)(n_steps[j] % cap) * (size_t)n + (size_t)j) * obs_dim, cur,
+                       sizeof(float) * obs_dim);
+            env_begin(&o, a);
+            const double total = robot_cycle_prologue(&o);
+            while (o.cycle_time < total && o.cycle_time < ct_stop[j]) {
+                robot_step(&o);
+                ++total_ticks;
+            }
+            o.pending = 1;
+        }
+        obj_pack(&o, state, n, j);
     }
     return total_ticks;
 }

@@ -1,0 +1,122 @@
+"""Sampled parity check of a chained rollout against the C oracle.
+
+TEST INFRASTRUCTURE ONLY (the checker, never the thing measured): used by
+tests/test_gpu_horizon.py and by bench.py after its timed region.
+
+After any number of `salp_rollout` launches every env i has completed
+steps_done[i] env-steps and may hold an in-flight cycle (pending, its
+cycle_time in the state).  Its whole history is a function of (seed, global
+id) alone, so the oracle replays a sample of env ids from creation
+(oracle_replay: reset, steps_done[i] random-action env-steps with auto-reset,
+then the in-flight cycle up to the device's cycle_time) and the device state
+and the last rollout-buffer rows must equal it bit for bit (NaN payloads
+aside: a diverged env's NaN goes through different instruction sequences;
+and -0 == +0, see _bits_differ; such values are counted separately).
+The reference path replayed: src/salp_robot_env.py:196-299 per env-step and
+src/robot.py:740-777 per cycle.
+"""
+import os
+
+import numpy as np
+
+from grasp_lab_salp_amd._abi import FIELD, NUM_FIELDS
+
+from . import oracle as orc
+
+HOT = slice(FIELD["v0"], FIELD["ang2"] + 1)
+
+
+def _threads():
+    return int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+
+
+def sample_ids(state, n, n_random=256, n_diverged=64, block=256, seed=0):
+    """Env ids to replay: the first and the last workgroup (256 envs each),
+    up to `n_diverged` envs whose kinematic state is non-finite, and
+    `n_random` others drawn uniformly."""
+    rng = np.random.default_rng(seed)
+    first = np.arange(min(block, n))
+    last = np.arange(max(n - block, 0), n)
+    bad = np.nonzero(~np.isfinite(state[HOT]).all(0))[0]
+    if len(bad) > n_diverged:
+        bad = np.sort(rng.choice(bad, n_diverged, replace=False))
+    rest = np.setdiff1d(np.arange(n), np.concatenate([first, last, bad]))
+    rnd = np.sort(rng.choice(rest, min(n_random, len(rest)), replace=False)) if len(rest) else rest
+    return np.unique(np.concatenate([first, last, bad, rnd])).astype(np.int64), bad
+
+
+def _bits_differ(a, b, zeros=True):
+    """Elementwise: the bit patterns differ, not both are NaN and (zeros) not
+    both are zeros.  The device drops terms that are exact zeros in the
+    reference's 3x3 products (salp_device.h header), so an all-zero sum (an
+    env at rest) may come out -0 where the oracle has +0; the value is the
+    same and nothing downstream tells them apart."""
+    a = np.ascontiguousarray(a)
+    b = np.ascontiguousarray(b)
+    iv = np.int64 if a.dtype == np.float64 else np.int32
+    if a.dtype.kind != "f":
+        return a != b
+    d = (a.view(iv) != b.view(iv)) & ~(np.isnan(a) & np.isnan(b))
+    return d & ~((a == 0) & (b == 0)) if zeros else d
+
+
+def check(state, steps_done, buffers, params, seed, env_offset=0, ids=None, threads=None, **sample_kw):
+    """Compare device results (numpy: state [NUM_FIELDS, n] float64, steps_done
+    [n] int64, buffers {obs, obs_before, actions, rewards, dones} with
+    [cap, n, ...] ring slots) with the oracle on sampled env ids.  Returns a
+    JSON-able summary; `ok` is True when everything matched."""
+    n = state.shape[1]
+    assert state.shape[0] == NUM_FIELDS
+    if ids is None:
+        ids, bad = sample_ids(state, n, **sample_kw)
+    else:
+        ids = np.asarray(ids, np.int64)
+        bad = ids[~np.isfinite(state[HOT][:, ids]).all(0)]
+    k = steps_done[ids].astype(np.int64)
+    pending = state[FIELD["pending"], ids] != 0.0
+    ct = np.where(pending, state[FIELD["cycle_time"], ids], -1.0)
+    cap = 0 if buffers is None else int(buffers["dones"].shape[0])
+    o_state, o_buf = orc.replay(ids + env_offset, k, ct, seed=seed, params=params, capacity=cap,
+                                threads=threads or _threads())
+    d = _bits_differ(state[:, ids], o_state)
+    signed_zero = int((_bits_differ(state[:, ids], o_state, zeros=False) & ~d).sum())
+    bad_fields = {}
+    for f in np.nonzero(d.any(1))[0]:
+        bad_fields[int(f)] = int(d[f].sum())
+    env_bad = d.any(0)
+    from grasp_lab_salp_amd._abi import FIELDS
+    examples = []
+    for j in np.nonzero(env_bad)[0][:4]:
+        for f in np.nonzero(d[:, j])[0][:6]:
+            dv, ov = float(state[f, ids[j]]), float(o_state[f, j])
+            examples.append({"env": int(ids[j]) + env_offset, "field": FIELDS[f], "device": dv.hex(),
+                             "oracle": ov.hex(), "steps_done": int(k[j]),
+                             "cycle_time": float(state[FIELD["cycle_time"], ids[j]])})
+    res = {"envs_checked": int(len(ids)), "diverged_checked": int(len(bad)),
+           "first_id": int(ids.min()) + env_offset, "last_id": int(ids.max()) + env_offset,
+           "env_steps_replayed": int(k.sum()), "steps_done_min": int(k.min()), "steps_done_max": int(k.max()),
+           "pending_checked": int(pending.sum()), "state_mismatch_envs": int(env_bad.sum()),
+           "state_mismatch_fields": bad_fields, "examples": examples,
+           "signed_zero_only_values": signed_zero}
+    if cap:
+        rows = 0
+        mism = 0
+        for slot in range(cap):
+            # slot holds env-step t = the last t < k with t % cap == slot
+            t = k - 1 - ((k - 1 - slot) % cap)
+            valid = (k > 0) & (t >= 0) & (t >= k - cap)
+            if not valid.any():
+                continue
+            cols = ids[valid]
+            for name in ("obs", "obs_before", "actions", "rewards", "dones"):
+                dv = buffers[name][slot][cols]
+                ov = o_buf[name][slot][valid]
+                dd = _bits_differ(dv, ov)
+                if dd.ndim > 1:
+                    dd = dd.any(-1)
+                mism += int(dd.sum())
+            rows += int(valid.sum())
+        res["buffer_rows_checked"] = rows
+        res["buffer_row_mismatches"] = mism
+    res["ok"] = res["state_mismatch_envs"] == 0 and res.get("buffer_row_mismatches", 0) == 0
+    return res

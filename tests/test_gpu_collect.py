@@ -63,7 +63,7 @@ def test_collect_replays_on_the_lockstep_path(n, n_steps, gamma):
     w = pack_policy(pol)
     bufs = _buffers(n_steps, n, env.obs_dim)
     ep_start = torch.ones(n, dtype=torch.float32, device="cuda")
-    last_obs = torch.full((n, env.obs_dim), -7.0, device="cuda")
+    last_obs = obs0.clone()   # in/out: the observation the first step is taken on
     ep_stats = torch.zeros(2, dtype=torch.float64, device="cuda")
     diverged = torch.zeros(1, dtype=torch.int64, device="cuda")
     env.collect(w, n_steps, bufs, ep_start, last_obs, ep_stats, diverged, noise_seed=99, gamma=gamma,

@@ -326,3 +326,20 @@ def test_make_vec_env_honours_a_custom_vec_env_cls():
     b = make_vec_env(_make_env, n_envs=8, vec_env_cls=Dummy)
     assert isinstance(b, SalpVecEnv) and b.num_envs == 8
     b.close()
+    # SB3 seeds env rank r's action space with seed + r on the per-env path
+    from grasp_lab_salp_amd.spaces import Box
+    s = make_vec_env(_make_env, n_envs=2, seed=7, start_index=3, vec_env_cls=ListVecEnv)
+    for r, e in enumerate(s.envs):
+        ref = Box(e.action_space.low, e.action_space.high, dtype=np.float32)
+        ref.seed(7 + 3 + r)
+        assert np.array_equal(e.action_space.sample(), ref.sample())
+        e.close()
+    # vec_env_kwargs the batched env cannot honour raise instead of being dropped;
+    # SubprocVecEnv's start_method has no meaning for one launch and is accepted
+    Subproc = type("SubprocVecEnv", (), {})
+    with pytest.raises(TypeError):
+        make_vec_env(_make_env, n_envs=4, vec_env_cls=Subproc, vec_env_kwargs={"context": "fork"})
+    c = make_vec_env(_make_env, n_envs=4, vec_env_cls=Subproc, vec_env_kwargs={"start_method": "fork",
+                                                                                 "infos": False})
+    assert isinstance(c, SalpVecEnv)
+    c.close()

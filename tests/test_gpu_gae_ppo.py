@@ -159,6 +159,36 @@ def test_diverged_envs_are_reset_without_bootstrap():
     assert torch.isfinite(st[FIELD["v0"]:FIELD["ang2"] + 1, :4]).all()
 
 
+def test_guard_sees_the_terminal_observation_of_an_ended_episode():
+    """the blow-up action on 4 of 8 envs with max_cycles = 1, so the
+    diverging step also ends the episode (time limit) and auto-reset already
+    replaced r.obs by the fresh observation.  The guard must judge the
+    terminal observation (as salp_collect does), zero the reward without a
+    bootstrap, and not reset those envs a second time."""
+    from grasp_lab_salp_amd._abi import FIELD, default_params
+    from grasp_lab_salp_amd.ppo import PPO, diverged_mask
+    from grasp_lab_salp_amd.vec_env import SalpVecEnv
+    env = SalpVecEnv(8, params=default_params(max_cycles=1), seed=0, infos=False)
+    model = PPO("MlpPolicy", env, n_steps=2, batch_size=16, n_epochs=1, seed=0)
+    sim = model.sim
+    sim.reset()
+    ep0 = sim.get_state()[FIELD["episode"]].clone()
+    act = torch.full((8, 3), 0.5, device="cuda")
+    act[:4] = torch.tensor([0.0904393, 0.06936062, -0.76570743], device="cuda")
+    r = sim.step(act, auto_reset=True, want_terminal_obs=True)
+    assert r.truncated.all()
+    assert diverged_mask(r.terminal_obs, torch.zeros(8, device="cuda")).tolist() == [True] * 4 + [False] * 4
+    assert torch.isfinite(r.obs).all()   # auto-reset observations
+    fresh = r.obs.clone()
+    rew, bad = model._reset_diverged(r, r.reward.float())
+    assert bad.tolist() == [True] * 4 + [False] * 4
+    assert torch.equal(rew[:4], torch.zeros(4, device="cuda"))
+    assert r.terminated[:4].all()           # no gamma * V(terminal_obs) bootstrap
+    # one reset per ended episode: the episode counter moved by exactly one
+    assert torch.equal(sim.get_state()[FIELD["episode"]], ep0 + 1)
+    assert torch.equal(r.obs, fresh)
+
+
 def test_timeout_bootstrap_in_collection():
     """max_cycles = 1: every env-step ends by the time limit, so every buffer
     reward is the env reward + gamma * V(terminal_obs) (SB3 collect_rollouts)."""

@@ -1,0 +1,68 @@
+"""Parity at the bench's own horizon (BASELINE.json configs[2], the headline).
+
+The exact bench workload: 65 536 envs, tick budget 8 192 per launch, chunk
+128, the default steady budget (q = 360), a 16-slot rollout buffer, 25
+launches (~310 env-steps per env: re-seating, steady ticks, settled waves,
+auto-resets and diverged envs all exercised).  Then ~800 sampled env ids
+(the first and the last workgroup, up to 64 diverged envs, 256 random ones)
+are replayed from creation on the OpenMP oracle for exactly the env-steps
+each completed plus its in-flight cycle (oracle/sampled.py), and the device
+state and the last 16 buffer rows must equal the oracle bit for bit (NaN
+payloads aside).  A max_cycles = 5 variant makes the 500-cycle timeout
+(src/salp_robot_env.py:268-276) fire every few env-steps, mid-launch, at
+full size.  Reference path: src/salp_robot_env.py:196-299,
+src/robot.py:740-777.
+"""
+import numpy as np
+import pytest
+import torch
+
+from grasp_lab_salp_amd._abi import FIELD, default_params
+from grasp_lab_salp_amd.batched_env import BatchedSalpEnv
+from oracle import sampled
+
+pytestmark = pytest.mark.gpu
+
+N = 65536
+SEED = 0
+
+
+def _run(params, launches, seed=SEED, tick_budget=8192, chunk=128, cap=16):
+    env = BatchedSalpEnv(N, params=params, seed=seed)
+    bufs = {"obs": torch.zeros((cap, N, env.obs_dim), dtype=torch.float32, device="cuda"),
+            "obs_before": torch.zeros((cap, N, env.obs_dim), dtype=torch.float32, device="cuda"),
+            "actions": torch.zeros((cap, N, 3), dtype=torch.float32, device="cuda"),
+            "rewards": torch.zeros((cap, N), dtype=torch.float32, device="cuda"),
+            "dones": torch.zeros((cap, N), dtype=torch.uint8, device="cuda")}
+    done = torch.zeros(N, dtype=torch.int64, device="cuda")
+    for _ in range(launches):
+        env.rollout(tick_budget, buffers=bufs, steps_done=done, chunk=chunk)
+    torch.cuda.synchronize()
+    st = env.get_state().cpu().numpy()
+    return st, done.cpu().numpy(), {k: v.cpu().numpy() for k, v in bufs.items()}
+
+
+def test_bench_horizon_sampled_envs_match_oracle():
+    p = default_params()
+    st, done, bufs = _run(p, 25)
+    assert done.min() > 200, "25 launches of 8192 ticks: hundreds of env-steps per env"
+    res = sampled.check(st, done, bufs, p, SEED)
+    print(res)
+    assert res["diverged_checked"] >= 32, "the bench horizon has thousands of diverged envs"
+    assert res["pending_checked"] > 100
+    assert res["buffer_rows_checked"] >= 16 * res["envs_checked"]
+    assert res["ok"], res
+
+
+def test_bench_horizon_with_timeouts_mid_launch():
+    """max_cycles = 5: every episode that does not end earlier is truncated at
+    its 5th env-step, so timeouts and auto-resets happen inside every launch."""
+    p = default_params(max_cycles=5)
+    st, done, bufs = _run(p, 8)
+    res = sampled.check(st, done, bufs, p, SEED)
+    print(res)
+    # every env has reset about every 5 env-steps
+    ep = st[FIELD["episode"]]
+    assert ep.min() >= done.min() // 5
+    assert (bufs["dones"] & 2).any(), "truncations in the buffer rows"
+    assert res["ok"], res

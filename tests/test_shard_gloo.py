@@ -16,7 +16,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from grasp_lab_salp_amd._abi import default_params
-from grasp_lab_salp_amd.shard import env_id_offset, reduce_run
+from grasp_lab_salp_amd.shard import env_id_offset, reduce_run, reduce_sums
 
 N_PER_RANK = 48
 STEPS = 3
@@ -46,8 +46,9 @@ def _worker(rank, world, port, q):
         rsum = [torch.empty(N_PER_RANK, dtype=torch.float64) for _ in range(world)]
         dist.all_gather(rsum, torch.from_numpy(rs))
         red = reduce_run(1.0 + rank, 100 * (rank + 1), 10.0 * (rank + 1), 5.0)
+        sums = reduce_sums([3 + rank, 1.25e7 + 0.5 * rank, 2 ** 40 + rank])
         if rank == 0:
-            q.put(("ok", torch.cat(parts, 1).numpy(), torch.cat(rsum).numpy(), red))
+            q.put(("ok", torch.cat(parts, 1).numpy(), torch.cat(rsum).numpy(), (red, sums)))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover - reported to the parent
@@ -64,6 +65,7 @@ def test_env_id_offset():
 
 def test_reduce_run_without_process_group():
     assert reduce_run(2.0, 10, 3.0, None) == (2.0, 10.0, 3.0, 0.0)
+    assert reduce_sums([3, 2.5]) == [3, 2.5]
 
 
 def test_two_rank_shards_equal_unsharded_run():
@@ -79,6 +81,10 @@ def test_two_rank_shards_equal_unsharded_run():
         p.join(timeout=120)
     assert status == "ok", state
     assert all(p.exitcode == 0 for p in procs)
+    red, sums = red
+    # counters summed exactly as ints, rates as floats (not truncated)
+    assert sums == [7, 2.5e7 + 0.5, 2 ** 41 + 1]
+    assert isinstance(sums[0], int) and isinstance(sums[1], float)
 
     from oracle.oracle import Oracle
     ref = Oracle(default_params(), world * N_PER_RANK, seed=SEED, env_offset=0)
