@@ -97,6 +97,9 @@ def parse(argv=None):
     ap.add_argument("--no-lockstep", action="store_true")
     ap.add_argument("--no-parity-check", action="store_true",
                     help="skip the sampled oracle replay after the timed region")
+    ap.add_argument("--no-ppo", action="store_true", help="skip the config-5 PPO leg")
+    ap.add_argument("--ppo-envs", type=int, default=32768, help="PPO leg: envs per GPU (BASELINE configs[4])")
+    ap.add_argument("--ppo-steps", type=int, default=256, help="PPO leg: n_steps per collection")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher + reductions only, gloo on the CPU, no GPU kernels")
     return ap.parse_args(argv)
@@ -196,6 +199,48 @@ def cpu_baseline(seconds):
                         "env_steps_per_sec": 3000 / sum(c["seconds"] for c in cfg1)},
             "note": "cores = the CPU share the GPU pool grants a one-GPU job (OMP_NUM_THREADS); "
                     "the interpreted Python reference itself does ~2.1 env-steps/s per core (SURVEY.md §6)"}
+
+
+def ppo_leg(a, rank, world, dev):
+    """BASELINE.json configs[4]: PPO on 32 768 envs per GPU with the HIP GAE
+    scan (the learner of src/train_robot_recurrent_ppo.py:85-107 with its
+    gamma / lambda / clip / epochs, MlpPolicy, SB3 semantics restated in
+    grasp_lab_salp_amd/ppo.py).  One untimed iteration (warm-up: graph
+    capture, allocator), then one timed iteration of collection (salp_collect
+    at n_steps >= 256: the policy inside the chained kernel), GAE and 10
+    epochs of minibatch updates (batch 32 768; one RCCL all-reduce of the
+    gradients per minibatch when world > 1).  value = env-steps of the timed
+    iteration over all ranks / its wall time (max over ranks); the split comes
+    from HIP events on the stream.  k_gae alone is timed against the HBM
+    roofline (12 B read + 8 B written per (step, env))."""
+    from grasp_lab_salp_amd.ppo import PPO
+    from grasp_lab_salp_amd.vec_env import SalpVecEnv
+    from tools.bench_ppo import gae_roofline
+    n, T = a.ppo_envs, a.ppo_steps
+    env = SalpVecEnv(n, seed=a.seed, env_id_offset=env_id_offset(rank, n), device=dev.index, infos=False)
+    model = PPO("MlpPolicy", env, n_steps=T, batch_size=32768, n_epochs=10, seed=a.seed, collect="auto")
+    model.learn(T * n)   # warm-up iteration
+    for k in model.timing:
+        model.timing[k] = 0.0
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    model.num_timesteps = 0
+    t0 = time.perf_counter()
+    model.learn(T * n)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    el_max, steps, _, _ = reduce_run(el, model.num_timesteps, 0.0, 0.0, device=dev)
+    gae = gae_roofline(T, n)
+    timing = {k: reduce_run(v, 0, 0.0, 0.0, device=dev)[0] for k, v in model.timing.items()}
+    env.close()
+    del model, env
+    torch.cuda.empty_cache()
+    return {"metric": "PPO env-steps/sec (collection + GAE + update), BASELINE configs[4]", "value": steps / el_max,
+            "unit": "env-steps/s", "n_envs_per_gpu": n, "n_steps": T, "batch_size": 32768, "n_epochs": 10,
+            "collect": "chained (salp_collect)" if T >= 256 else "lockstep (salp_step)",
+            "iteration_s": el_max, "timing_s_max_over_ranks": timing,
+            "gae_kernel": gae, "policy": "SB3 MlpPolicy 64-64 tanh (the reference's RecurrentPPO uses LSTM-256)"}
 
 
 def dry_run(a, world, rank):
@@ -340,6 +385,12 @@ def main(argv=None):
         given = 4 * n / timed(lambda: [env.step(x, auto_reset=True) for x in acts])
         chained32 = 32 * n / timed(lambda: env.step_random(32))
 
+    ppo = None
+    if not a.no_ppo:
+        del bufs
+        torch.cuda.empty_cache()
+        ppo = ppo_leg(a, rank, world, dev)
+
     elapsed, steps_total, kern_ms, lock_total = reduce_run(elapsed, steps_local, kern_ms, lock, device=dev)
     given_total = reduce_sums([given or 0.0], device=dev)[0] if given is not None else None
     chained32_total = reduce_sums([chained32 or 0.0], device=dev)[0] if chained32 is not None else None
@@ -423,6 +474,8 @@ def main(argv=None):
                         "Newton steps of divisions and polynomial transcendentals included"}
     if parity is not None:
         res["parity_sampled"] = parity
+    if ppo is not None:
+        res["ppo"] = ppo
     if world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(a.cpu_baseline_seconds)
     print(json.dumps(res), flush=True)

@@ -202,7 +202,8 @@ class BatchedSalpEnv:
         obs, actions, rewards, episode_starts, values, log_probs (SB3's
         RolloutBuffer fields); ``episode_start`` [n] f32 in/out, ``last_obs``
         [n, obs_dim] in/out (in: the observation each env's first step is
-        taken on, e.g. the one reset() returned), ``ep_stats`` [2] f64 and ``diverged`` [1] i64
+        taken on, e.g. the one reset() returned), ``ep_stats`` [4] f64 (return, episodes,
+        successes, length sums) and ``diverged`` [1] i64
         accumulated.  See include/salp.h for the exact semantics."""
         R = _lib.SalpPolicyRollout()
         w = weights
@@ -219,7 +220,7 @@ class BatchedSalpEnv:
             setattr(R, k, t.data_ptr())
         for name, t, dt, shp in (("episode_start", episode_start, torch.float32, (self.n_envs,)),
                                  ("last_obs", last_obs, torch.float32, (self.n_envs, self.obs_dim)),
-                                 ("ep_stats", ep_stats, torch.float64, (2,)),
+                                 ("ep_stats", ep_stats, torch.float64, (4,)),
                                  ("diverged", diverged, torch.int64, (1,))):
             if t.dtype != dt or tuple(t.shape) != shp or not t.is_contiguous() or t.device != self.device:
                 raise ValueError(f"{name} must be a contiguous {dt} tensor of shape {shp} on {self.device}")

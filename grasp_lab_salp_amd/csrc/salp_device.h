@@ -639,8 +639,18 @@ SD bool next_tick_steady(const Hot& h, const Params& P) {
  * branch that uses it, not at the top of the tick (no register round trip;
  * faster in k_rollout, slower in the lock-step kernels: A/B in
  * profiles/r1f_experiments.md). */
-template <bool REC = false, bool RAND = false, bool LATE32 = false, bool STEADY = false>
-SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_t rs = 0) {
+/* SETTLED (with STEADY): the tick after a steady tick that ended settled
+ * (tick's return value): the values that are then exactly +0 are used as
+ * the constants they are — centre-of-mass rate and acceleration, water-mass
+ * rate and jet speed (settled), the inertia rate I - prev_I (a steady tick
+ * set prev_I = I and kept I), and the jet force (the previous steady tick's
+ * update_state gave COAST or REST) — and the arithmetic that produced them is
+ * skipped.  Every remaining operation is the same, so the results are bit
+ * for bit those of the plain steady tick; and the tick ends settled again.
+ * Returns, for a STEADY tick, whether this lane is settled after it. */
+template <bool REC = false, bool RAND = false, bool LATE32 = false, bool STEADY = false, bool SETTLED = false>
+SD bool tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_t rs = 0) {
+    static_assert(!SETTLED || STEADY, "a settled tick is a steady one");
     /* this cycle's float32-mode geometry, used at the end if the lane is in
      * that mode (issued first so that the LDS latency hides under the tick) */
     double k32[C32_N];
@@ -681,23 +691,24 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     double df1 = sm_mad(g.kc1 * h.v1, dfr, g.kc1 * vn * h.v1);
     double df2 = sm_mad(g.kc1 * h.v2, dfr, g.kc1 * vn * h.v2);
     /* jet force, JET phase only (src/robot.py:937-951, src/dynamics.py:87-101) */
-    const bool jet = h.phase == JET;
+    const bool jet = !SETTLED && h.phase == JET;
     double jf0 = jet ? g.mr * (h.d0 * g.speed) * -cd : 0.0;
     double jf1 = jet ? g.mr * (h.d1 * g.speed) * -cd : 0.0;
     double jf2 = jet ? g.mr * (h.d2 * g.speed) * -cd : 0.0;
     /* added-mass force (src/dynamics.py:131-141) */
+    const double mr = SETTLED ? 0.0 : g.mr;
     double am0 = m * cam0, am1 = m * cam1, am2 = m * cam2;
-    double amr0 = g.mr * car0, amr1 = g.mr * car1, amr2 = g.mr * car2;
+    double amr0 = mr * car0, amr1 = mr * car1, amr2 = mr * car2;
     double amv0 = am0 * h.v0, amv1 = am1 * h.v1, amv2 = am2 * h.v2;
     double af0 = -sm_mad(amr0, h.v0, sm_mad(am0, h.a0, cross_c(h.w1, amv2, h.w2, amv1)));
     double af1 = -sm_mad(amr1, h.v1, sm_mad(am1, h.a1, cross_c(h.w2, amv0, h.w0, amv2)));
     double af2 = -sm_mad(amr2, h.v2, sm_mad(am2, h.a2, cross_c(h.w0, amv1, h.w1, amv0)));
     /* fictitious forces of the moving center of mass (src/robot.py:806-810);
      * com = (cx, 0, 0) */
-    const double cx = h.com, crx = h.comr;
+    const double cx = h.com, crx = SETTLED ? 0.0 : h.comr;
     double acc_y = (h.w0 * (h.w1 * cx) + (h.w2 * crx) * 2.0) + h.al2 * cx;
     double acc_z = (h.w0 * (h.w2 * cx) + -(h.w1 * crx) * 2.0) + -(h.al1 * cx);
-    double acc_x = cross_c(h.w1, -(h.w1 * cx), h.w2, h.w2 * cx) + h.coma;
+    double acc_x = cross_c(h.w1, -(h.w1 * cx), h.w2, h.w2 * cx) + (SETTLED ? 0.0 : h.coma);
     /* total force and linear acceleration (src/dynamics.py:5-10) */
     double na0, na1, na2;
     const Rcp rm{m, g.rm};
@@ -724,11 +735,15 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     /* jet torque r x F, r = (mid_x - L/2, 0, 0) (src/robot.py:931-935) */
     double jt1 = -(g.rx * jf2), jt2 = g.rx * jf1;
     /* deformation torque -(dI/dt) w; prev_I <- I (src/robot.py:888-896) */
-    double ir0 = div_dt(I0 - h.pI0), ir1 = div_dt(I1 - h.pI1);
-    double ir2 = ir1;
-    if (h.pI2 != h.pI1) ir2 = div_dt(I1 - h.pI2);   /* prev_I[1,1] == prev_I[2,2] always */
+    double ir0 = 0.0, ir1 = 0.0, ir2 = 0.0;   /* settled: (I - prev_I) / dt = +0 / dt */
+    if (!SETTLED) {
+        ir0 = div_dt(I0 - h.pI0);
+        ir1 = div_dt(I1 - h.pI1);
+        ir2 = ir1;
+        if (h.pI2 != h.pI1) ir2 = div_dt(I1 - h.pI2);   /* prev_I[1,1] == prev_I[2,2] always */
+        h.pI0 = I0; h.pI1 = I1; h.pI2 = I1;
+    }
     double dft0 = -(ir0 * h.w0), dft1 = -(ir1 * h.w1), dft2 = -(ir2 * h.w2);
-    h.pI0 = I0; h.pI1 = I1; h.pI2 = I1;
     /* added-mass torque, I_rate term identically zero (src/dynamics.py:144-156) */
     double at0 = I0 * cat0, at1 = I1 * cat1, at2 = I1 * cat2;
     double atw0 = at0 * h.w0, atw1 = at1 * h.w1, atw2 = at2 * h.w2;
@@ -797,16 +812,25 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     /* ---------------- clocks, phase, properties ---------------- */
     h.ct += DT;
     h.time += DT;
-    {   /* update_state's if-chain as flat selects, lowest priority first */
+    if (STEADY) {
+        /* A steady tick's cycle_time is past mx and mx + jet (next_tick_steady
+         * checked this very sum), so update_state gives COAST or REST and
+         * body_lw the float64 rest body (init_length, init_width) the lane
+         * already holds (next_tick_steady: L == L0, W == W0, !g32). */
+        h.phase = h.ct <= h.b2 ? COAST : REST;
+        h.pV = h.V;
+        h.pv32 = false;
+    } else {
+        /* update_state's if-chain as flat selects, lowest priority first */
         int ph = h.ct <= h.b2 ? COAST : REST;
         ph = h.ct <= h.b1 ? JET : ph;
         h.phase = h.ct <= h.mx ? REFILL : ph;
+        h.pV = h.V;
+        h.pv32 = h.g32;
+        bool f;
+        body_lw(P, h.phase, h.ct, h.refill, h.mx, h.c, h.cr, h.rr, h.c32, &h.L, &h.W, &f);
+        h.g32 = f;
     }
-    h.pV = h.V;
-    h.pv32 = h.g32;
-    bool f;
-    body_lw(P, h.phase, h.ct, h.refill, h.mx, h.c, h.cr, h.rr, h.c32, &h.L, &h.W, &f);
-    h.g32 = f;
     if (STEADY) {
         /* Steady body (see next_tick_steady): update_properties recomputes
          * the previous tick's volume, water mass, centre of mass, mass,
@@ -817,9 +841,12 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
         /* From the second steady tick on these are all +0 and recompute as +0
          * (V == pV, pv32 == false, com - com = +0, and div_dt / qdiv of +0 is
          * +0), so a wave whose lanes are all there skips them. */
-        const bool settled = (__double_as_longlong(h.comr) | __double_as_longlong(h.coma) |
-                              __double_as_longlong(h.geo.mr) | __double_as_longlong(h.geo.speed)) == 0;
-        if (!__all(settled)) {
+        if (SETTLED) return true;
+        const auto zero = [&] {
+            return (__double_as_longlong(h.comr) | __double_as_longlong(h.coma) | __double_as_longlong(h.geo.mr) |
+                    __double_as_longlong(h.geo.speed)) == 0;
+        };
+        if (!__all(zero())) {
             const double comr = div_dt(h.com - h.com);
             h.coma = div_dt(comr - h.comr);
             h.comr = comr;
@@ -828,7 +855,7 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
             h.geo.mr = div_dt(water_mass(P, h.V, false) - pwm);
             h.geo.speed = qdiv(div_dt(h.V - h.pV), rcp_of(P.nozzle_area));
         }
-        return;
+        return zero();
     }
     /* float64 geometry (bitwise the f = false instance of the shared code),
      * replaced by the cycle's float32 geometry where the lane is in that mode */
@@ -837,6 +864,7 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     double wm = water_mass(P, V, false);
     double com = center_of_mass(P, c, wm, false);
     Geo ng = make_geo_shape(P, c, h.L, h.W, wm, false);
+    const bool f = h.g32;
     if (f) {
         if (LATE32)
             for (int k = 0; k < C32_N; ++k) k32[k] = c32[k];
@@ -853,6 +881,7 @@ SD void tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     jet_rates(P, V, h.pV, wm, f, h.pv32, ng);
     geo_recips(ng);
     h.geo = ng;
+    return false;
 }
 
 /* ------------------------------------------- Nozzle / Robot control */

@@ -49,7 +49,14 @@ __device__ __forceinline__ void run_cycle(Hot& h, const Params& P, salp::Cache32
         if (__all(salp::next_tick_steady(h, PV))) break;
         salp::tick<false, RAND>(h, PV, c32);
     }
-    for (; h.ct < h.b2 && g < kMaxTicksPerCycle; ++g) salp::tick<false, RAND, false, true>(h, PV, c32);
+    // steady ticks until the wave's lanes are settled (salp_device.h tick), then settled ones
+    for (; h.ct < h.b2 && g < kMaxTicksPerCycle; ++g) {
+        if (__all(salp::tick<false, RAND, false, true>(h, PV, c32))) {
+            ++g;
+            break;
+        }
+    }
+    for (; h.ct < h.b2 && g < kMaxTicksPerCycle; ++g) salp::tick<false, RAND, false, true, true>(h, PV, c32);
 }
 
 // The loop of Robot.step_through_cycle with record=True (src/robot.py:
@@ -397,6 +404,8 @@ __device__ __forceinline__ void rollout_boundary(Hot& h, ST S, const Params& P, 
                 if (reset && !bad) {
                     atomicAdd(&R.ep_stats[0], SF(SALP_F_EP_RETURN));
                     atomicAdd(&R.ep_stats[1], 1.0);
+                    if (r.terminated) atomicAdd(&R.ep_stats[2], 1.0);   // the target was reached
+                    atomicAdd(&R.ep_stats[3], SF(SALP_F_EP_LEN));
                 }
                 R.rewards[row] = rew;
                 reset = reset || bad;
@@ -668,8 +677,19 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
             if (h.ct < h.b2) salp::tick<false, RAND, true>(h, PV, c32);
         }
         const int32_t ks = (int32_t)(((int64_t)(A.chunk - k) * A.steady_q8) >> 8);
-        for (int32_t j = 0; j < ks; ++j)
-            if (h.ct < h.b2) salp::tick<false, RAND, true, true>(h, PV, c32);
+        // steady ticks until every ticking lane of the wave is settled, then
+        // settled ticks (salp_device.h tick; lanes whose cycle has ended idle)
+        int32_t j = 0;
+        for (; j < ks; ++j) {
+            bool settled = true;
+            if (h.ct < h.b2) settled = salp::tick<false, RAND, true, true>(h, PV, c32);
+            if (__all(settled)) {
+                ++j;
+                break;
+            }
+        }
+        for (; j < ks; ++j)
+            if (h.ct < h.b2) salp::tick<false, RAND, true, true, true>(h, PV, c32);
     }
     if (A.B.steps_done && i < P.n) A.B.steps_done[i] = steps;
 }

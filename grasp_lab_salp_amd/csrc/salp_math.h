@@ -85,7 +85,7 @@ SM_QUAL float sm_fmaf(float a, float b, float c) { return fmaf(a, b, c); }
  * device and the oracle are always built in the same mode, so they agree bit
  * for bit in either. */
 #ifndef SALP_FMA
-#define SALP_FMA 0
+#define SALP_FMA 1
 #endif
 SM_QUAL double sm_mad(double a, double b, double c) {
 #if SALP_FMA

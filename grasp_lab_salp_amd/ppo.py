@@ -142,6 +142,7 @@ class _FusedPPOLossFn(torch.autograd.Function):
 
 _PPO_WS = 2048   # include/salp.h SALP_PPO_WORKSPACE_DOUBLES
 _EP_RETURN = INFO["ep_return"]
+_EP_LEN = INFO["ep_len"]
 
 
 def ppo_loss(mu, log_std, value, actions, old_logp, advantages, returns, clip_range, ent_coef, vf_coef,
@@ -388,8 +389,9 @@ class PPO:
         self.verbose = verbose
         self.reset_nonfinite = reset_nonfinite
         self._nonfinite = torch.zeros((), dtype=torch.int64, device=self.device)
-        # finished-episode statistics of the current collection (device, sync-free)
-        self._ep_stats = torch.zeros(2, dtype=torch.float64, device=self.device)
+        # finished-episode statistics of the current collection (device, sync-free):
+        # return sum, episodes, successes (target reached: terminated), length sum
+        self._ep_stats = torch.zeros(4, dtype=torch.float64, device=self.device)
         # minibatch permutations are drawn on the device: SB3 permutes on the
         # host (np.random.permutation), which at n_steps 2048 x 32 768 envs is
         # a 537 MB index array per epoch to build and upload
@@ -437,6 +439,7 @@ class PPO:
             a, v, lp = pol.act(obs, generator=self.sample_gen)
             r = sim.step(torch.clamp(a, self.low, self.high), auto_reset=True, want_terminal_obs=True)
             rew = r.reward.float()
+            reached = r.terminated.clone()   # the task's own termination: target reached
             bad = None
             if self.reset_nonfinite:
                 rew, bad = self._reset_diverged(r, rew)
@@ -447,9 +450,10 @@ class PPO:
             rew = timeout_bootstrap(rew, r.terminated, r.truncated, tv, self.gamma)
             done = (r.terminated | r.truncated)
             ended = done if bad is None else done & ~bad    # episodes that ended by the task's rules
-            ep_ret = r.info[:, _EP_RETURN]
-            self._ep_stats += torch.stack([torch.where(ended, ep_ret, torch.zeros_like(ep_ret)).sum(),
-                                           ended.sum().double()])
+            ep_ret, ep_len = r.info[:, _EP_RETURN], r.info[:, _EP_LEN]
+            zero = torch.zeros_like(ep_ret)
+            self._ep_stats += torch.stack([torch.where(ended, ep_ret, zero).sum(), ended.sum().double(),
+                                           (ended & reached).sum().double(), torch.where(ended, ep_len, zero).sum()])
             b.obs[t].copy_(obs)
             b.actions[t].copy_(a)
             b.rewards[t].copy_(rew)
@@ -632,9 +636,11 @@ class PPO:
             self.timing["train_s"] += ev[2].elapsed_time(end) / 1e3
             self.num_timesteps += self.n_steps * self.n_envs
             it += 1
-            ret_sum, n_ep = self._ep_stats.tolist()
+            ret_sum, n_ep, n_succ, len_sum = self._ep_stats.tolist()
             row = {"iteration": len(self.history) + 1, "timesteps": self.num_timesteps, **self.logger,
                    "episodes": int(n_ep), "ep_return_mean": ret_sum / n_ep if n_ep else None,
+                   "success_rate": n_succ / n_ep if n_ep else None,
+                   "ep_len_mean": len_sum / n_ep if n_ep else None,
                    "diverged_envs": int(self._nonfinite - div0)}
             self.history.append(row)
             if self.verbose and it % log_interval == 0:

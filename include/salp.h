@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define SALP_ABI_VERSION 5
+#define SALP_ABI_VERSION 6
 
 #define SALP_MAX_OBSTACLES 4
 #define SALP_OBS_DIM_MAX (6 + 2 * SALP_MAX_OBSTACLES)
@@ -193,7 +193,8 @@ int salp_step_random(SalpEnv* h, int32_t n_steps, double* reward_sum_out, void* 
  * call is taken on (the reset observation, or the previous call's last_obs);
  * on return episode_start[i] (next step starts an episode) and last_obs[i]
  * (the obs after the last step, the reset obs where it ended an episode).
- * ep_stats[0..1] += (return, 1) per episode that ended by the task's rules;
+ * ep_stats[0..3] += (return, 1, target reached (terminated), length) per
+ * episode that ended by the task's rules;
  * diverged[0] += envs reset by the guard. */
 typedef struct SalpPolicyRollout {
     const float* weights;  /* [SALP_POLICY_SIZE] */
@@ -210,7 +211,7 @@ typedef struct SalpPolicyRollout {
     float* log_probs;      /* [n_steps][n_envs]           */
     float* episode_start;  /* [n_envs] in/out             */
     float* last_obs;       /* [n_envs][obs_dim] in/out    */
-    double* ep_stats;      /* [2] accumulated             */
+    double* ep_stats;      /* [4] accumulated             */
     int64_t* diverged;     /* [1] accumulated             */
 } SalpPolicyRollout;
 int salp_collect(SalpEnv* h, const SalpPolicyRollout* r, void* stream);

@@ -64,7 +64,7 @@ def test_collect_replays_on_the_lockstep_path(n, n_steps, gamma):
     bufs = _buffers(n_steps, n, env.obs_dim)
     ep_start = torch.ones(n, dtype=torch.float32, device="cuda")
     last_obs = obs0.clone()   # in/out: the observation the first step is taken on
-    ep_stats = torch.zeros(2, dtype=torch.float64, device="cuda")
+    ep_stats = torch.zeros(4, dtype=torch.float64, device="cuda")
     diverged = torch.zeros(1, dtype=torch.int64, device="cuda")
     env.collect(w, n_steps, bufs, ep_start, last_obs, ep_stats, diverged, noise_seed=99, gamma=gamma,
                 diverged_obs_abs=DIVERGED_OBS_ABS, diverged_reward_abs=DIVERGED_REWARD_ABS)
@@ -87,7 +87,7 @@ def test_collect_replays_on_the_lockstep_path(n, n_steps, gamma):
     # the environment side, replayed lock-step on the twin
     obs = obs0
     starts = torch.ones(n, dtype=torch.float32, device="cuda")
-    stats = np.zeros(2)
+    stats = np.zeros(4)
     n_bad = n_trunc = 0
     for t in range(n_steps):
         assert _equal_up_to_nan_payload(_cpu(bufs["obs"][t]), _cpu(obs)), t
@@ -107,7 +107,8 @@ def test_collect_replays_on_the_lockstep_path(n, n_steps, gamma):
         assert _equal_up_to_nan_payload(_cpu(got[nb]), _cpu(want[nb])), t
         assert torch.allclose(got[boot], rew32[boot] + np.float32(gamma) * tv[boot], rtol=1e-6, atol=1e-5), t
         ended = done & ~bad
-        stats += [float(r.info[ended, INFO["ep_return"]].sum()), float(ended.sum())]
+        stats += [float(r.info[ended, INFO["ep_return"]].sum()), float(ended.sum()),
+                  float((ended & r.terminated.bool()).sum()), float(r.info[ended, INFO["ep_len"]].sum())]
         fresh = twin.reset(mask=bad & ~done)
         obs = torch.where((bad & ~done).unsqueeze(1), fresh, r.obs)
         starts = (done | bad).float()
@@ -127,7 +128,7 @@ def test_collect_rejects_bad_buffers():
     w = pack_policy(pol)
     bufs = _buffers(4, 64, env.obs_dim)
     args = (torch.ones(64, device="cuda"), torch.zeros((64, env.obs_dim), device="cuda"),
-            torch.zeros(2, dtype=torch.float64, device="cuda"), torch.zeros(1, dtype=torch.int64, device="cuda"))
+            torch.zeros(4, dtype=torch.float64, device="cuda"), torch.zeros(1, dtype=torch.int64, device="cuda"))
     with pytest.raises(ValueError):
         env.collect(w[:-1], 4, bufs, *args)
     bad = dict(bufs, values=torch.zeros((4, 63), device="cuda"))

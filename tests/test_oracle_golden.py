@@ -15,6 +15,11 @@ the step outputs.  Tolerances are stated per quantity:
 * the roll channel (w0, alpha0, angle0, ...) is identically zero in exact
   arithmetic — only rounding noise of order 1e-20 — so it is compared with an
   absolute tolerance.
+
+Both arithmetic modes of the restatement are pinned (salp_math.h SALP_FMA):
+"numpy" (SALP_FMA=0, NumPy's unfused products and sums: most values
+bit-identical to the reference) and "fma" (the mode libsalp.so is built in:
+products fused into the sums that consume them), to the same tolerances.
 """
 import numpy as np
 import pytest
@@ -40,15 +45,23 @@ def golden():
     return load_episodes()
 
 
+MODES = {"fma": False, "numpy": True}   # mode -> Oracle(exact=...)
+
+
+@pytest.fixture(scope="module", params=sorted(MODES))
+def mode(request):
+    return request.param
+
+
 @pytest.fixture(scope="module")
-def replay(golden):
+def replay(golden, mode):
     """Oracle teacher-forced on every fixture row (grouped by obstacle count)."""
     d = golden
     rows = np.arange(len(d["job_index"]))
     out = []
     for K in np.unique(d["num_obstacles_cfg"]):
         sel = rows[d["num_obstacles_cfg"] == K]
-        o = Oracle(default_params(num_obstacles=int(K)), len(sel))
+        o = Oracle(default_params(num_obstacles=int(K)), len(sel), exact=MODES[mode])
         o.state[:] = snapshot_to_state(d, "b_", sel)
         res = o.step(d["action"][sel])
         out.append((int(K), sel, o.state.copy(), snapshot_to_state(d, "a_", sel), res))
@@ -89,7 +102,7 @@ def test_minimal_state_invariants(golden):
         assert np.array_equal(pwm, d[p + "r_prev_water_mass"])
 
 
-def test_teacher_forced_state(replay):
+def test_teacher_forced_state(replay, mode):
     got = np.concatenate([r[2] for r in replay], axis=1)
     ref = np.concatenate([r[3] for r in replay], axis=1)
     for name in COMPARED:
@@ -102,9 +115,10 @@ def test_teacher_forced_state(replay):
             e = _scaled(got[i], ref[i])
             tol = OUT_OF_PLANE_TOL if name in OUT_OF_PLANE else STATE_TOL
             assert np.max(e) <= tol, (name, float(np.max(e)))
-    # the bulk of rows are bit-identical to the reference
+    # the bulk of rows are bit-identical to the reference (NumPy's own
+    # roundings); fusing products into sums moves about a third of them by an ulp
     dyn = [FIELD[n] for n in ("pw0", "pw1", "v0", "v1", "eta2", "w2")]
-    assert np.mean(got[dyn] == ref[dyn]) > 0.75
+    assert np.mean(got[dyn] == ref[dyn]) > (0.75 if mode == "numpy" else 0.5)
 
 
 def test_teacher_forced_outputs(replay, golden):
@@ -151,10 +165,11 @@ def test_monitor_episode_return(golden):
     assert o is not None
 
 
-def test_tick_trace():
+@pytest.mark.parametrize("exact", [False, True], ids=["fma", "numpy"])
+def test_tick_trace(exact):
     """Per-tick histories (record=True) of a bare robot for four cycles."""
     t = load_trace()
-    o = robot_trace(t["actions"])
+    o = robot_trace(t["actions"], exact=exact)
     assert o.shape[0] == len(t["length_history"])
     # geometry: equal except one-ulp effects of the IK angles through turn_time
     for col, key in ((21, "length_history"), (22, "width_history"), (23, "volume_history"),
@@ -200,7 +215,8 @@ def free_run(sim_step, sim_reset_to, d, job):
     return eo, er
 
 
-def test_free_running_episodes_match_reference(golden):
+@pytest.mark.parametrize("exact", [False, True], ids=["fma", "numpy"])
+def test_free_running_episodes_match_reference(golden, exact):
     """Every fixture episode replayed WITHOUT teacher forcing (the oracle's own
     state carried from step to step, 10-503 env-steps): observations within
     1e-5 relative (measured: 2.5e-7), rewards within 1e-4, identical flags."""
@@ -208,7 +224,7 @@ def test_free_running_episodes_match_reference(golden):
     for job in np.unique(d["job_index"]):
         rows = np.where(d["job_index"] == job)[0]
         K = int(d["num_obstacles_cfg"][rows[0]])
-        o = Oracle(default_params(num_obstacles=K), 1)
+        o = Oracle(default_params(num_obstacles=K), 1, exact=exact)
         o.state[:] = snapshot_to_state(d, "b_", rows[:1])
         eo, er = free_run(o.step, o.reset_to, d, job)
         assert eo <= FREE_RUN_OBS_TOL, (job, eo)

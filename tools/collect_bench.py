@@ -30,7 +30,7 @@ def main():
         z = lambda *s: torch.zeros(s, dtype=torch.float32, device="cuda")  # noqa: E731
         bufs = {"obs": z(k, n, env.obs_dim), "actions": z(k, n, 3), "rewards": z(k, n), "episode_starts": z(k, n),
                 "values": z(k, n), "log_probs": z(k, n)}
-        extra = (torch.ones(n, device="cuda"), z(n, env.obs_dim), torch.zeros(2, dtype=torch.float64, device="cuda"),
+        extra = (torch.ones(n, device="cuda"), z(n, env.obs_dim), torch.zeros(4, dtype=torch.float64, device="cuda"),
                  torch.zeros(1, dtype=torch.int64, device="cuda"))
         out = {"n_envs": n, "k": k}
         for rep in range(2):

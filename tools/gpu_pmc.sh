@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-r1}
-ARGS=${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --no-lockstep}
+ARGS=${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --no-lockstep --no-parity-check --no-ppo}
 PASSES=${PASSES:-fetch write waves mix}
 pass() {  # name counters...
     local name=$1

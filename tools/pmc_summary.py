@@ -42,7 +42,7 @@ def main():
     out = {"tag": a.tag, "kernel": a.kernel,
            "config": {"n_envs": a.n_envs, "tick_budget": a.tick_budget, "chunk": a.chunk},
            "command": "tools/gpu_pmc.sh: rocprofv3 --pmc <group> --kernel-trace -- python3 bench.py "
-                      "--steps 2 --warmup 1 --no-cpu-baseline --no-lockstep, one pass per group",
+                      "--steps 2 --warmup 1 --no-cpu-baseline --no-lockstep --no-parity-check --no-ppo, one pass per group",
            "per_dispatch": per, "derived": {}}
     d = out["derived"]
     if g("FETCH_SIZE") is not None:
