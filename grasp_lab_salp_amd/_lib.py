@@ -56,6 +56,48 @@ class SalpPolicyRollout(ctypes.Structure):
     ]
 
 
+N_MLP_TENSORS = 13   # include/salp.h SALP_MLP_N_TENSORS
+
+
+class SalpPpoMinibatch(ctypes.Structure):
+    _fields_ = [
+        ("batch", ctypes.c_int64),
+        ("obs_dim", ctypes.c_int32),
+        ("normalize_advantage", ctypes.c_int32),
+        ("idx", ctypes.c_void_p),
+        ("obs", ctypes.c_void_p),
+        ("actions", ctypes.c_void_p),
+        ("old_log_prob", ctypes.c_void_p),
+        ("advantages", ctypes.c_void_p),
+        ("returns", ctypes.c_void_p),
+        ("params", ctypes.c_void_p * N_MLP_TENSORS),
+        ("grads", ctypes.c_void_p),
+        ("clip_range", ctypes.c_double),
+        ("ent_coef", ctypes.c_double),
+        ("vf_coef", ctypes.c_double),
+        ("workspace", ctypes.c_void_p),
+        ("stats", ctypes.c_void_p),
+    ]
+
+
+class SalpPpoAdam(ctypes.Structure):
+    _fields_ = [
+        ("obs_dim", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("params", ctypes.c_void_p * N_MLP_TENSORS),
+        ("grads", ctypes.c_void_p),
+        ("exp_avg", ctypes.c_void_p),
+        ("exp_avg_sq", ctypes.c_void_p),
+        ("step", ctypes.c_void_p),
+        ("grad_norm", ctypes.c_void_p),
+        ("lr", ctypes.c_double),
+        ("beta1", ctypes.c_double),
+        ("beta2", ctypes.c_double),
+        ("eps", ctypes.c_double),
+        ("max_grad_norm", ctypes.c_double),
+    ]
+
+
 class SalpTraceBuffer(ctypes.Structure):
     _fields_ = [
         ("max_samples", ctypes.c_int64),
@@ -101,6 +143,11 @@ SIGNATURES = {
                                 ctypes.c_double, _V, _V, _V]),
     "salp_ppo_loss": (ctypes.c_int, [ctypes.c_int64, _V, _V, _V, _V, _V, _V, _V, ctypes.c_double, ctypes.c_double,
                                      ctypes.c_double, ctypes.c_int, _V, _V, _V, _V, _V]),
+    "salp_ppo_mlp_num_params": (ctypes.c_int64, [ctypes.c_int]),
+    "salp_ppo_mlp_offset": (ctypes.c_int64, [ctypes.c_int, ctypes.c_int]),
+    "salp_ppo_mlp_workspace_doubles": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int]),
+    "salp_ppo_mlp_grads": (ctypes.c_int, [ctypes.POINTER(SalpPpoMinibatch), _V]),
+    "salp_ppo_mlp_apply": (ctypes.c_int, [ctypes.POINTER(SalpPpoAdam), _V]),
 }
 
 

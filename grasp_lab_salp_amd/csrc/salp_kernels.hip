@@ -912,13 +912,15 @@ int launched(SalpEnv* h, const char* what) { return check_hip(h, hipGetLastError
 unsigned blocks_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 // k_rollout's steady ticks per full tick of a wave's chunk budget (x256): a
-// steady tick costs ~0.8 of a full one in this kernel (profiles/r2_experiments.md r2l-r2o).
+// steady tick costs ~0.8 of a full one in the round-2 kernel (q = 360,
+// profiles/r2_experiments.md r2l-r2o); with the fused arithmetic and settled
+// ticks ~0.65 (q = 480 best of 360..580, profiles/r3_experiments.md r3f).
 // SALP_STEADY_Q8 overrides it for tuning runs; it changes throughput only.
 int32_t rollout_steady_q8() {
     static const int32_t q = [] {
         const char* e = std::getenv("SALP_STEADY_Q8");
         const long v = e ? std::strtol(e, nullptr, 10) : 0;
-        return (int32_t)(v > 0 && v < (1 << 16) ? v : 360);
+        return (int32_t)(v > 0 && v < (1 << 16) ? v : 480);
     }();
     return q;
 }
@@ -976,6 +978,14 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t salp_ppo_loss_launch
     const float* old_logp, const float* adv, const float* returns, double clip_range, double ent_coef,
     double vf_coef, int normalize_advantage, double* workspace, float* out, float* dmu, float* dvalue,
     void* stream);
+
+extern "C" __attribute__((visibility("hidden"))) int64_t salp_ppo_mlp_params_impl(int obs_dim);
+extern "C" __attribute__((visibility("hidden"))) int64_t salp_ppo_mlp_offset_impl(int obs_dim, int tensor);
+extern "C" __attribute__((visibility("hidden"))) int64_t salp_ppo_mlp_workspace_impl(int64_t batch, int obs_dim);
+extern "C" __attribute__((visibility("hidden"))) hipError_t salp_ppo_mlp_grads_launch(const SalpPpoMinibatch* m,
+                                                                                       void* stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t salp_ppo_mlp_apply_launch(const SalpPpoAdam* a,
+                                                                                       void* stream);
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t salp_sort_temp_bytes(int64_t n, size_t* bytes);
 extern "C" __attribute__((visibility("hidden"))) hipError_t salp_sort_launch(
@@ -1337,6 +1347,41 @@ int salp_ppo_loss(int64_t batch, const float* mu, const float* log_std, const fl
                                               clip_range, ent_coef, vf_coef, normalize_advantage, workspace, out, dmu,
                                               dvalue, stream);
     return check_hip(nullptr, e, "k_ppo");
+}
+
+int64_t salp_ppo_mlp_num_params(int obs_dim) {
+    return (obs_dim > 0 && obs_dim <= SALP_OBS_DIM_MAX) ? salp_ppo_mlp_params_impl(obs_dim) : -1;
+}
+int64_t salp_ppo_mlp_offset(int obs_dim, int tensor) {
+    if (obs_dim <= 0 || obs_dim > SALP_OBS_DIM_MAX || tensor < 0 || tensor > SALP_MLP_N_TENSORS) return -1;
+    return salp_ppo_mlp_offset_impl(obs_dim, tensor);
+}
+int64_t salp_ppo_mlp_workspace_doubles(int64_t batch, int obs_dim) {
+    if (batch <= 0 || obs_dim <= 0 || obs_dim > SALP_OBS_DIM_MAX) return -1;
+    return salp_ppo_mlp_workspace_impl(batch, obs_dim);
+}
+
+int salp_ppo_mlp_grads(const SalpPpoMinibatch* m, void* stream) {
+    if (!m || m->batch <= 0) return fail(nullptr, SALP_EINVAL, "salp_ppo_mlp_grads: batch must be positive");
+    if (m->obs_dim <= 0 || m->obs_dim > SALP_OBS_DIM_MAX)
+        return fail(nullptr, SALP_EINVAL, "salp_ppo_mlp_grads: obs_dim out of range");
+    if (!m->idx || !m->obs || !m->actions || !m->old_log_prob || !m->advantages || !m->returns || !m->grads ||
+        !m->workspace)
+        return fail(nullptr, SALP_EINVAL, "salp_ppo_mlp_grads: null buffer");
+    for (int t = 0; t < SALP_MLP_N_TENSORS; ++t)
+        if (!m->params[t]) return fail(nullptr, SALP_EINVAL, "salp_ppo_mlp_grads: null parameter tensor");
+    if (!(m->clip_range >= 0)) return fail(nullptr, SALP_EINVAL, "salp_ppo_mlp_grads: clip_range must be >= 0");
+    return check_hip(nullptr, salp_ppo_mlp_grads_launch(m, stream), "k_mlp");
+}
+
+int salp_ppo_mlp_apply(const SalpPpoAdam* a, void* stream) {
+    if (!a || a->obs_dim <= 0 || a->obs_dim > SALP_OBS_DIM_MAX)
+        return fail(nullptr, SALP_EINVAL, "salp_ppo_mlp_apply: obs_dim out of range");
+    if (!a->grads || !a->exp_avg || !a->exp_avg_sq || !a->step)
+        return fail(nullptr, SALP_EINVAL, "salp_ppo_mlp_apply: null buffer");
+    for (int t = 0; t < SALP_MLP_N_TENSORS; ++t)
+        if (!a->params[t]) return fail(nullptr, SALP_EINVAL, "salp_ppo_mlp_apply: null parameter tensor");
+    return check_hip(nullptr, salp_ppo_mlp_apply_launch(a, stream), "k_mlp_apply");
 }
 
 int salp_gae(int64_t n_steps, int64_t n_envs, const float* rewards, const float* values,

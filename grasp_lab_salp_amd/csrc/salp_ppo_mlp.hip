@@ -1,0 +1,512 @@
+// salp_ppo_mlp.hip — one PPO minibatch step of the built-in MlpPolicy, fused
+// (gfx950).
+//
+// What it replaces: the minibatch step of stable_baselines3 PPO.train
+// (stable-baselines3 >= 2.0, requirements.txt:6-7) for SB3's MlpPolicy
+// (separate 64-64 tanh actor and critic, diagonal Gaussian with
+// state-independent log-std), as grasp_lab_salp_amd/ppo.py runs it with torch
+// ops: forward of both networks, the clipped-surrogate / value / entropy loss
+// (salp_ppo.hip's head), backward, clip_grad_norm_(max_norm) and Adam.  In
+// torch that is ~60 small kernels per minibatch (GEMMs, elementwise, reduce,
+// foreach); here it is four launches:
+//
+//   k_mlp_adv_sums   block partials of sum(adv), sum(adv^2) over the gathered
+//                    rows (the advantage normalisation's mean / std)
+//   k_mlp_fwd_bwd    every block takes a contiguous slice of the minibatch in
+//                    tiles of 64 rows: forward through both networks (weights
+//                    and activations in LDS, 4x4 register tiles), the loss
+//                    head per row, backward to the weight gradients, which
+//                    the block accumulates in registers over its tiles and
+//                    writes as one fp32 partial per parameter
+//   k_mlp_reduce     sums the partials in fp64 into the flat gradient, and
+//                    the loss statistics
+//   k_mlp_apply      (salp_ppo_mlp_apply) the global gradient norm, the
+//                    clipping coefficient and Adam, in one block
+//
+// Between the last two a multi-GPU learner all-reduces the flat gradient
+// (one RCCL message).  Row math is float32 like torch's; reductions are fp64;
+// the results agree with torch to float32 rounding (tests/test_gpu_ppo_mlp.py),
+// not bit for bit (different summation orders), and are deterministic (no
+// atomics).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "../../include/salp.h"
+
+namespace {
+
+constexpr int H = SALP_POLICY_HIDDEN;   // 64 hidden units per layer
+constexpr int NA = 3;                   // action dims
+constexpr int DP = 16;                  // observation columns in LDS (SALP_OBS_DIM_MAX <= 16)
+constexpr int TR = 64;                  // rows per tile
+constexpr int NT = 512;                 // threads per block of the row kernel (8 waves)
+constexpr int HS = H + 1;               // LDS row stride of the activations (bank spread)
+constexpr int NB_MAX = 256;             // row blocks (partials) at most
+constexpr int NADV = 256;               // blocks of k_mlp_adv_sums
+constexpr int NSTAT = 6;                // stats partials: pg, vf, clip, d log_std x 3
+constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
+static_assert(SALP_OBS_DIM_MAX <= DP, "observation columns fit the LDS tile");
+
+// Offsets of the tensors in the flat gradient / Adam-state layout.
+struct Layout {
+    int64_t off[SALP_MLP_N_TENSORS + 1];
+};
+__host__ __device__ inline int64_t tensor_size(int t, int d) {
+    switch (t) {
+        case SALP_MLP_PI_W1: case SALP_MLP_VF_W1: return (int64_t)H * d;
+        case SALP_MLP_PI_W2: case SALP_MLP_VF_W2: return (int64_t)H * H;
+        case SALP_MLP_ACT_W: return (int64_t)NA * H;
+        case SALP_MLP_ACT_B: case SALP_MLP_LOG_STD: return NA;
+        case SALP_MLP_VAL_W: return H;
+        case SALP_MLP_VAL_B: return 1;
+        default: return H;   // hidden-layer biases
+    }
+}
+__host__ __device__ inline Layout make_layout(int d) {
+    Layout L;
+    L.off[0] = 0;
+    for (int t = 0; t < SALP_MLP_N_TENSORS; ++t) L.off[t + 1] = L.off[t] + tensor_size(t, d);
+    return L;
+}
+
+struct RowArgs {
+    SalpPpoMinibatch m;
+    Layout L;
+    int64_t rows_per_block;   // multiple of TR
+    float* part;              // [gridDim.x][n_params]
+    double* stat_part;        // [gridDim.x][NSTAT]
+    const double* adv_part;   // [NADV][2]
+};
+
+__device__ __forceinline__ double block_sum_d(double v, double* sh, int nthreads) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int w = threadIdx.x / 64, l = threadIdx.x % 64;
+    __syncthreads();
+    if (l == 0) sh[w] = v;
+    __syncthreads();
+    double t = 0.0;
+    if (threadIdx.x == 0)
+        for (int k = 0; k < nthreads / 64; ++k) t += sh[k];
+    __syncthreads();
+    return t;   // valid in thread 0
+}
+
+__global__ __launch_bounds__(256) void k_mlp_adv_sums(int64_t B, const int64_t* __restrict__ idx,
+                                                      const float* __restrict__ adv, double* __restrict__ part) {
+    __shared__ double sh[4];
+    double s = 0.0, q = 0.0;
+    for (int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x; b < B; b += (int64_t)gridDim.x * 256) {
+        const double x = adv[idx[b]];
+        s += x;
+        q += x * x;
+    }
+    s = block_sum_d(s, sh, 256);
+    q = block_sum_d(q, sh, 256);
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = s;
+        part[2 * blockIdx.x + 1] = q;
+    }
+}
+
+__global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
+    const SalpPpoMinibatch& m = a.m;
+    const int D = m.obs_dim;
+    const int64_t B = m.batch;
+    const int tid = threadIdx.x;
+    // weights (nets: 0 = actor / pi, 1 = critic / vf)
+    __shared__ float sW1[2][H][DP];       // [net][unit][input]
+    __shared__ float sB1[2][H];
+    __shared__ float sW2T[2][H][H];       // [net][input k][unit j]   (forward)
+    __shared__ float sW2[2][H][H];        // [net][unit j][input k]   (dh1 = W2^T dz2)
+    __shared__ float sB2[2][H];
+    __shared__ float sAw[NA][H], sAb[NA], sLs[NA], sVw[H], sVb;
+    // one tile of rows
+    __shared__ float sX[TR][DP];
+    __shared__ float sH1[2][TR][HS];      // h1, then dz1 in place
+    __shared__ float sH2[2][TR][HS];      // h2, then dz2 in place
+    __shared__ float sDmu[TR][NA], sDv[TR];
+    __shared__ float sNorm[2];
+    __shared__ double sRed[NT / 64];
+
+    for (int e = tid; e < 2 * H * DP; e += NT) {
+        const int net = e / (H * DP), u = (e / DP) % H, k = e % DP;
+        const float* w = m.params[net ? SALP_MLP_VF_W1 : SALP_MLP_PI_W1];
+        sW1[net][u][k] = k < D ? w[u * D + k] : 0.0f;
+    }
+    for (int e = tid; e < 2 * H * H; e += NT) {
+        const int net = e / (H * H), j = (e / H) % H, k = e % H;
+        const float w = m.params[net ? SALP_MLP_VF_W2 : SALP_MLP_PI_W2][j * H + k];
+        sW2T[net][k][j] = w;
+        sW2[net][j][k] = w;
+    }
+    for (int e = tid; e < 2 * H; e += NT) {
+        const int net = e / H, j = e % H;
+        sB1[net][j] = m.params[net ? SALP_MLP_VF_B1 : SALP_MLP_PI_B1][j];
+        sB2[net][j] = m.params[net ? SALP_MLP_VF_B2 : SALP_MLP_PI_B2][j];
+    }
+    for (int e = tid; e < NA * H; e += NT) sAw[e / H][e % H] = m.params[SALP_MLP_ACT_W][e];
+    if (tid < H) sVw[tid] = m.params[SALP_MLP_VAL_W][tid];
+    if (tid < NA) {
+        sAb[tid] = m.params[SALP_MLP_ACT_B][tid];
+        sLs[tid] = m.params[SALP_MLP_LOG_STD][tid];
+    }
+    if (tid == 0) {
+        sVb = m.params[SALP_MLP_VAL_B][0];
+        float mean = 0.0f, inv = 1.0f;
+        if (m.normalize_advantage && B > 1) {
+            double s = 0.0, q = 0.0;
+            for (int k = 0; k < NADV; ++k) { s += a.adv_part[2 * k]; q += a.adv_part[2 * k + 1]; }
+            const double mu = s / (double)B;
+            const double var = fmax(q - s * mu, 0.0) / (double)(B - 1);
+            mean = (float)mu;
+            inv = 1.0f / ((float)sqrt(var) + 1e-8f);
+        }
+        sNorm[0] = mean;
+        sNorm[1] = inv;
+    }
+    __syncthreads();
+
+    // GEMM thread mapping: half the block per network, 16 x 16 groups of 4 x 4
+    const int net = tid / 256, tt = tid % 256, g4a = (tt / 16) * 4, g4b = (tt % 16) * 4;
+    // gradient accumulators, kept over the block's tiles
+    float gW2[4][4] = {};      // dW2[net][g4a + i][g4b + c]   (unit j, input k)
+    float gB2[4] = {};         // db2[net][g4a + i]            (threads with g4b == 0)
+    float gW1[4] = {};         // dW1 entries e = tid + q * NT of the [2][H][DP] layout
+    float gB1 = 0.0f;          // db1[tid / H][tid % H]          (threads < 2 H)
+    float gHead = 0.0f;        // dWa (tid < 192), dVw (192 <= tid < 256)
+    float gHeadB = 0.0f;       // dab (256 <= tid < 259), dvb (tid == 259)
+    double st[NSTAT] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    float ls[NA], var[NA];
+    for (int j = 0; j < NA; ++j) {
+        ls[j] = sLs[j];
+        const float sd = expf(ls[j]);
+        var[j] = sd * sd;
+    }
+    const float invB = 1.0f / (float)B, clip = (float)m.clip_range, vfc = (float)m.vf_coef;
+    const float amean = sNorm[0], ainv = sNorm[1];
+    const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_block;
+    const int64_t r_end = r_begin + a.rows_per_block < B ? r_begin + a.rows_per_block : B;
+
+    for (int64_t row0 = r_begin; row0 < r_end; row0 += TR) {
+        const int nrows = (int)(r_end - row0 < TR ? r_end - row0 : TR);
+        // ---- observations of the tile (gathered rows; padding rows are zero)
+        for (int e = tid; e < TR * DP; e += NT) {
+            const int r = e / DP, k = e % DP;
+            sX[r][k] = (r < nrows && k < D) ? m.obs[m.idx[row0 + r] * D + k] : 0.0f;
+        }
+        __syncthreads();
+        // ---- layer 1: h1 = tanh(W1 x + b1)
+        {
+            float acc[4][4];
+            for (int i = 0; i < 4; ++i)
+                for (int c = 0; c < 4; ++c) acc[i][c] = sB1[net][g4b + c];
+            for (int k = 0; k < D; ++k) {
+                float x[4], w[4];
+                for (int i = 0; i < 4; ++i) x[i] = sX[g4a + i][k];
+                for (int c = 0; c < 4; ++c) w[c] = sW1[net][g4b + c][k];
+                for (int i = 0; i < 4; ++i)
+                    for (int c = 0; c < 4; ++c) acc[i][c] = fmaf(x[i], w[c], acc[i][c]);
+            }
+            for (int i = 0; i < 4; ++i)
+                for (int c = 0; c < 4; ++c) sH1[net][g4a + i][g4b + c] = tanhf(acc[i][c]);
+        }
+        __syncthreads();
+        // ---- layer 2: h2 = tanh(W2 h1 + b2)
+        {
+            float acc[4][4];
+            for (int i = 0; i < 4; ++i)
+                for (int c = 0; c < 4; ++c) acc[i][c] = sB2[net][g4b + c];
+            for (int k = 0; k < H; ++k) {
+                float x[4];
+                for (int i = 0; i < 4; ++i) x[i] = sH1[net][g4a + i][k];
+                const float4 w = *reinterpret_cast<const float4*>(&sW2T[net][k][g4b]);
+                for (int i = 0; i < 4; ++i) {
+                    acc[i][0] = fmaf(x[i], w.x, acc[i][0]);
+                    acc[i][1] = fmaf(x[i], w.y, acc[i][1]);
+                    acc[i][2] = fmaf(x[i], w.z, acc[i][2]);
+                    acc[i][3] = fmaf(x[i], w.w, acc[i][3]);
+                }
+            }
+            for (int i = 0; i < 4; ++i)
+                for (int c = 0; c < 4; ++c) sH2[net][g4a + i][g4b + c] = tanhf(acc[i][c]);
+        }
+        __syncthreads();
+        // ---- heads and the loss head: 8 threads per row
+        {
+            const int r = tid / 8, p = tid % 8;
+            float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            for (int q = 0; q < 8; ++q) {
+                const int j = p * 8 + q;
+                const float hp = sH2[0][r][j], hv = sH2[1][r][j];
+                s[0] = fmaf(hp, sAw[0][j], s[0]);
+                s[1] = fmaf(hp, sAw[1][j], s[1]);
+                s[2] = fmaf(hp, sAw[2][j], s[2]);
+                s[3] = fmaf(hv, sVw[j], s[3]);
+            }
+            for (int o = 1; o < 8; o <<= 1)
+                for (int c = 0; c < 4; ++c) s[c] += __shfl_xor(s[c], o, 64);
+            if (p == 0) {
+                float dmu[NA] = {0.0f, 0.0f, 0.0f}, dv = 0.0f;
+                if (r < nrows) {
+                    const int64_t b = m.idx[row0 + r];
+                    float d[NA], lp = 0.0f;
+                    for (int j = 0; j < NA; ++j) {
+                        const float mu = s[j] + sAb[j];
+                        d[j] = m.actions[3 * b + j] - mu;
+                        lp += -(d[j] * d[j]) / (2.0f * var[j]) - ls[j] - kLogSqrt2Pi;
+                    }
+                    const float v = s[3] + sVb;
+                    const float adv = m.advantages[b];
+                    const float A = m.normalize_advantage ? (adv - amean) * ainv : adv;
+                    const float rt = expf(lp - m.old_log_prob[b]);
+                    const float rc = fminf(fmaxf(rt, 1.0f - clip), 1.0f + clip);
+                    const float p1 = A * rt, p2 = A * rc;
+                    const float g1 = p1 < p2 ? 1.0f : (p1 == p2 ? 0.5f : 0.0f);
+                    const float g2 = p2 < p1 ? 1.0f : (p1 == p2 ? 0.5f : 0.0f);
+                    const bool inside = rt >= 1.0f - clip && rt <= 1.0f + clip;
+                    const float dL_dr = g1 * A + (inside ? g2 * A : 0.0f);
+                    const float dlp = -invB * dL_dr * rt;
+                    for (int j = 0; j < NA; ++j) {
+                        dmu[j] = dlp * d[j] / var[j];
+                        st[3 + j] += (double)(dlp * (d[j] * d[j] / var[j] - 1.0f));
+                    }
+                    const float e = m.returns[b] - v;
+                    dv = vfc * (-2.0f * e * invB);
+                    st[0] += (double)fminf(p1, p2);
+                    st[1] += (double)(e * e);
+                    st[2] += fabsf(rt - 1.0f) > clip ? 1.0 : 0.0;
+                }
+                for (int j = 0; j < NA; ++j) sDmu[r][j] = dmu[j];
+                sDv[r] = dv;
+            }
+        }
+        __syncthreads();
+        // ---- head gradients (read h2 before dz2 overwrites it)
+        if (tid < NA * H) {
+            const int c = tid / H, j = tid % H;
+            float acc = 0.0f;
+            for (int r = 0; r < TR; ++r) acc = fmaf(sDmu[r][c], sH2[0][r][j], acc);
+            gHead += acc;
+        } else if (tid < NA * H + H) {
+            const int j = tid - NA * H;
+            float acc = 0.0f;
+            for (int r = 0; r < TR; ++r) acc = fmaf(sDv[r], sH2[1][r][j], acc);
+            gHead += acc;
+        } else if (tid < NA * H + H + NA + 1) {
+            const int c = tid - NA * H - H;
+            float acc = 0.0f;
+            for (int r = 0; r < TR; ++r) acc += c < NA ? sDmu[r][c] : sDv[r];
+            gHeadB += acc;
+        }
+        __syncthreads();
+        // ---- dz2 = (head^T d) * (1 - h2^2), in place
+        for (int e = tid; e < 2 * TR * H; e += NT) {
+            const int n = e / (TR * H), r = (e / H) % TR, j = e % H;
+            const float h = sH2[n][r][j];
+            const float dh = n == 0 ? fmaf(sDmu[r][2], sAw[2][j], fmaf(sDmu[r][1], sAw[1][j], sDmu[r][0] * sAw[0][j]))
+                                    : sDv[r] * sVw[j];
+            sH2[n][r][j] = dh * (1.0f - h * h);
+        }
+        __syncthreads();
+        // ---- dW2 += dz2^T h1, db2 += sum dz2 (4x4 tile: units g4a.., inputs g4b..)
+        for (int r = 0; r < TR; ++r) {
+            float z[4], x[4];
+            for (int i = 0; i < 4; ++i) z[i] = sH2[net][r][g4a + i];
+            for (int c = 0; c < 4; ++c) x[c] = sH1[net][r][g4b + c];
+            for (int i = 0; i < 4; ++i)
+                for (int c = 0; c < 4; ++c) gW2[i][c] = fmaf(z[i], x[c], gW2[i][c]);
+            if (g4b == 0)
+                for (int i = 0; i < 4; ++i) gB2[i] += z[i];
+        }
+        __syncthreads();
+        // ---- dh1 = W2^T dz2, dz1 = dh1 (1 - h1^2) in place (rows g4a.., inputs g4b..)
+        {
+            float acc[4][4] = {};
+            for (int j = 0; j < H; ++j) {
+                float z[4];
+                for (int i = 0; i < 4; ++i) z[i] = sH2[net][g4a + i][j];
+                const float4 w = *reinterpret_cast<const float4*>(&sW2[net][j][g4b]);
+                for (int i = 0; i < 4; ++i) {
+                    acc[i][0] = fmaf(z[i], w.x, acc[i][0]);
+                    acc[i][1] = fmaf(z[i], w.y, acc[i][1]);
+                    acc[i][2] = fmaf(z[i], w.z, acc[i][2]);
+                    acc[i][3] = fmaf(z[i], w.w, acc[i][3]);
+                }
+            }
+            // only this thread's own h1 entries are read and replaced here (the
+            // dW2 pass that read every h1 ended at the barrier above)
+            for (int i = 0; i < 4; ++i)
+                for (int c = 0; c < 4; ++c) {
+                    const float h = sH1[net][g4a + i][g4b + c];
+                    sH1[net][g4a + i][g4b + c] = acc[i][c] * (1.0f - h * h);
+                }
+        }
+        __syncthreads();
+        // ---- dW1 += dz1^T x, db1 += sum dz1
+        for (int q = 0; q < (2 * H * DP) / NT; ++q) {
+            const int e = tid + q * NT;
+            const int n = e / (H * DP), u = (e / DP) % H, k = e % DP;
+            if (k < D) {
+                float acc = 0.0f;
+                for (int r = 0; r < TR; ++r) acc = fmaf(sH1[n][r][u], sX[r][k], acc);
+                gW1[q] += acc;
+            }
+        }
+        if (tid < 2 * H) {
+            const int n = tid / H, u = tid % H;
+            float acc = 0.0f;
+            for (int r = 0; r < TR; ++r) acc += sH1[n][r][u];
+            gB1 += acc;
+        }
+        __syncthreads();
+    }
+
+    // ---- this block's partials, in the flat gradient layout
+    float* P = a.part + (int64_t)blockIdx.x * a.L.off[SALP_MLP_N_TENSORS];
+    {
+        const int64_t ow2 = a.L.off[net ? SALP_MLP_VF_W2 : SALP_MLP_PI_W2];
+        for (int i = 0; i < 4; ++i)
+            for (int c = 0; c < 4; ++c) P[ow2 + (g4a + i) * H + g4b + c] = gW2[i][c];
+        if (g4b == 0) {
+            const int64_t ob2 = a.L.off[net ? SALP_MLP_VF_B2 : SALP_MLP_PI_B2];
+            for (int i = 0; i < 4; ++i) P[ob2 + g4a + i] = gB2[i];
+        }
+    }
+    for (int q = 0; q < (2 * H * DP) / NT; ++q) {
+        const int e = tid + q * NT;
+        const int n = e / (H * DP), u = (e / DP) % H, k = e % DP;
+        if (k < D) P[a.L.off[n ? SALP_MLP_VF_W1 : SALP_MLP_PI_W1] + u * D + k] = gW1[q];
+    }
+    if (tid < 2 * H) P[a.L.off[tid / H ? SALP_MLP_VF_B1 : SALP_MLP_PI_B1] + tid % H] = gB1;
+    if (tid < NA * H) P[a.L.off[SALP_MLP_ACT_W] + tid] = gHead;
+    else if (tid < NA * H + H) P[a.L.off[SALP_MLP_VAL_W] + tid - NA * H] = gHead;
+    else if (tid < NA * H + H + NA) P[a.L.off[SALP_MLP_ACT_B] + tid - NA * H - H] = gHeadB;
+    else if (tid == NA * H + H + NA) P[a.L.off[SALP_MLP_VAL_B]] = gHeadB;
+    for (int k = 0; k < NSTAT; ++k) {
+        const double t = block_sum_d(st[k], sRed, NT);
+        if (tid == 0) a.stat_part[(int64_t)blockIdx.x * NSTAT + k] = t;
+    }
+}
+
+// Flat gradient = sum of the block partials (fp64); d loss / d log_std gets its
+// row sums and - ent_coef; block 0 also adds the loss statistics to stats[4].
+__global__ __launch_bounds__(256) void k_mlp_reduce(SalpPpoMinibatch m, Layout L, int nb, const float* part,
+                                                    const double* stat_part) {
+    const int64_t P = L.off[SALP_MLP_N_TENSORS];
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t ols = L.off[SALP_MLP_LOG_STD];
+    if (p < P) {
+        double s = 0.0;
+        if (p >= ols && p < ols + NA) {
+            for (int b = 0; b < nb; ++b) s += stat_part[(int64_t)b * NSTAT + 3 + (p - ols)];
+            s = (double)((float)s - (float)m.ent_coef);
+        } else {
+            for (int b = 0; b < nb; ++b) s += (double)part[(int64_t)b * P + p];
+        }
+        m.grads[p] = (float)s;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && m.stats) {
+        double t[3] = {0.0, 0.0, 0.0};
+        for (int b = 0; b < nb; ++b)
+            for (int k = 0; k < 3; ++k) t[k] += stat_part[(int64_t)b * NSTAT + k];
+        const double B = (double)m.batch;
+        float ent = 0.0f;
+        for (int j = 0; j < NA; ++j) ent += 0.5f + kLogSqrt2Pi + m.params[SALP_MLP_LOG_STD][j];
+        m.stats[0] += (float)(-t[0] / B);   // pg_loss
+        m.stats[1] += (float)(t[1] / B);    // vf_loss
+        m.stats[2] += ent;                  // entropy
+        m.stats[3] += (float)(t[2] / B);    // clip fraction
+    }
+}
+
+// clip_grad_norm_(max_norm) and torch.optim.Adam (no weight decay, no
+// amsgrad), over the flat gradient, in one block.
+constexpr int NT_APPLY = 1024;
+__global__ __launch_bounds__(NT_APPLY) void k_mlp_apply(SalpPpoAdam o, Layout L) {
+    __shared__ double sh[NT_APPLY / 64];
+    __shared__ float s_coef, s_step;
+    const int64_t P = L.off[SALP_MLP_N_TENSORS];
+    double q = 0.0;
+    for (int64_t p = threadIdx.x; p < P; p += NT_APPLY) {
+        const double g = o.grads[p];
+        q += g * g;
+    }
+    q = block_sum_d(q, sh, NT_APPLY);
+    if (threadIdx.x == 0) {
+        const float total = (float)sqrt(q);
+        float coef = 1.0f;
+        if (o.max_grad_norm > 0.0) {
+            coef = (float)o.max_grad_norm / (total + 1e-6f);
+            coef = coef < 1.0f ? coef : 1.0f;
+        }
+        s_coef = coef;
+        s_step = o.step[0] + 1.0f;
+        if (o.grad_norm) o.grad_norm[0] = total;
+    }
+    __syncthreads();
+    const float coef = s_coef, step = s_step;
+    const float b1 = (float)o.beta1, b2 = (float)o.beta2, lr = (float)o.lr, eps = (float)o.eps;
+    const float bc1 = 1.0f - powf(b1, step), bc2 = 1.0f - powf(b2, step);
+    const float step_size = lr / bc1, bc2_sqrt = sqrtf(bc2);
+    for (int t = 0; t < SALP_MLP_N_TENSORS; ++t) {
+        float* w = o.params[t];
+        for (int64_t i = threadIdx.x; i < L.off[t + 1] - L.off[t]; i += NT_APPLY) {
+            const int64_t p = L.off[t] + i;
+            const float g = o.grads[p] * coef;
+            const float m = b1 * o.exp_avg[p] + (1.0f - b1) * g;
+            const float v = b2 * o.exp_avg_sq[p] + (1.0f - b2) * g * g;
+            o.exp_avg[p] = m;
+            o.exp_avg_sq[p] = v;
+            w[i] -= step_size * m / (sqrtf(v) / bc2_sqrt + eps);
+        }
+    }
+    if (threadIdx.x == 0) o.step[0] = step;
+}
+
+}  // namespace
+
+extern "C" __attribute__((visibility("hidden"))) int64_t salp_ppo_mlp_params_impl(int obs_dim) {
+    return make_layout(obs_dim).off[SALP_MLP_N_TENSORS];
+}
+extern "C" __attribute__((visibility("hidden"))) int64_t salp_ppo_mlp_offset_impl(int obs_dim, int tensor) {
+    return make_layout(obs_dim).off[tensor];
+}
+
+// Blocks of the row kernel and the workspace they need (doubles).
+static int row_blocks(int64_t B) {
+    const int64_t tiles = (B + TR - 1) / TR;
+    return (int)(tiles < NB_MAX ? tiles : NB_MAX);
+}
+extern "C" __attribute__((visibility("hidden"))) int64_t salp_ppo_mlp_workspace_impl(int64_t B, int obs_dim) {
+    const int nb = row_blocks(B);
+    const int64_t P = make_layout(obs_dim).off[SALP_MLP_N_TENSORS];
+    // adv partials, stats partials (doubles) + fp32 parameter partials (as doubles, rounded up)
+    return 2 * NADV + (int64_t)nb * NSTAT + ((int64_t)nb * P + 1) / 2;
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t salp_ppo_mlp_grads_launch(const SalpPpoMinibatch* mb,
+                                                                                       void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const SalpPpoMinibatch& m = *mb;
+    const int nb = row_blocks(m.batch);
+    const Layout L = make_layout(m.obs_dim);
+    double* adv_part = m.workspace;
+    double* stat_part = adv_part + 2 * NADV;
+    float* part = reinterpret_cast<float*>(stat_part + (int64_t)nb * NSTAT);
+    hipLaunchKernelGGL(k_mlp_adv_sums, dim3(NADV), dim3(256), 0, s, m.batch, m.idx, m.advantages, adv_part);
+    const int64_t tiles = (m.batch + TR - 1) / TR;
+    const int64_t rpb = (tiles + nb - 1) / nb * TR;
+    RowArgs a{m, L, rpb, part, stat_part, adv_part};
+    hipLaunchKernelGGL(k_mlp_fwd_bwd, dim3(nb), dim3(NT), 0, s, a);
+    const int64_t P = L.off[SALP_MLP_N_TENSORS];
+    hipLaunchKernelGGL(k_mlp_reduce, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, m, L, nb, part, stat_part);
+    return hipGetLastError();
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t salp_ppo_mlp_apply_launch(const SalpPpoAdam* o,
+                                                                                       void* stream) {
+    hipLaunchKernelGGL(k_mlp_apply, dim3(1), dim3(NT_APPLY), 0, (hipStream_t)stream, *o, make_layout(o->obs_dim));
+    return hipGetLastError();
+}

@@ -21,9 +21,11 @@ scan (HIP kernel ``salp_gae``) and the policy all stay in HBM:
 * multi-GPU: one process per GPU, each with its own env shard; gradients are
   averaged with one flat all-reduce per minibatch (torch.distributed, ``nccl``
   = RCCL over xGMI; the MLP's gradients are ~20 KB, so one bucket);
-* single GPU: the whole minibatch update (forward, backward, clipping, Adam)
-  is captured into a HIP graph once per update and replayed per minibatch;
-  the small MLP is otherwise bound by ~60 kernel launches per step.
+* update: for the built-in policy the whole minibatch step (forward, loss,
+  backward, clipping, Adam) is four HIP kernels (``salp_ppo_mlp_grads`` /
+  ``salp_ppo_mlp_apply``, csrc/salp_ppo_mlp.hip) instead of ~60 torch kernels;
+  on one GPU it is captured into a HIP graph once and replayed per minibatch;
+  other policies take the torch path (autograd, torch Adam, a graph per update).
 
 The policy is SB3's ``MlpPolicy`` for PPO (separate 64-64 tanh actor and critic,
 orthogonal init, state-independent log-std).  The reference's RecurrentPPO
@@ -344,7 +346,7 @@ class PPO:
     def __init__(self, policy, env, learning_rate=3e-4, n_steps=2048, batch_size=64, n_epochs=10, gamma=0.99,
                  gae_lambda=0.95, clip_range=0.2, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5,
                  normalize_advantage=True, seed=0, device=None, verbose=0, reset_nonfinite=True,
-                 use_graphs=None, fused_loss=None, collect="auto"):
+                 use_graphs=None, fused_loss=None, collect="auto", fused_update=None):
         if policy not in ("MlpPolicy", None) and not isinstance(policy, nn.Module):
             raise ValueError("policy must be 'MlpPolicy' or an nn.Module")
         if fused_loss and isinstance(policy, nn.Module) and not all(
@@ -376,6 +378,7 @@ class PPO:
                                     capturable=self.use_graphs, fused=fused or None)
         self._graph = None
         self._graph_warm = 0
+        self._g_clip = None
         self.n_steps, self.batch_size, self.n_epochs = int(n_steps), int(batch_size), int(n_epochs)
         # clip_range may be an SB3-style schedule: f(progress_remaining) -> value
         self.gamma, self.gae_lambda, self.clip_range = gamma, gae_lambda, clip_range
@@ -386,6 +389,16 @@ class PPO:
         # built-in policy on a GPU; torch ops otherwise (custom policies)
         self.fused_loss = (self.device.type == "cuda" and isinstance(self.policy, ActorCritic)
                            if fused_loss is None else bool(fused_loss))
+        # the whole minibatch step (forward, loss, backward, clipping, Adam) as
+        # the HIP kernels of salp_ppo_mlp_grads / salp_ppo_mlp_apply for the
+        # built-in policy on a GPU; torch ops + torch Adam otherwise
+        if fused_update and not isinstance(self.policy, ActorCritic):
+            raise ValueError("fused_update=True runs the built-in ActorCritic (64-64 tanh MlpPolicy) only")
+        self.fused_update = (self.device.type == "cuda" and isinstance(self.policy, ActorCritic)
+                             and self.policy.pi_net[0].out_features == 64 if fused_update is None
+                             else bool(fused_update))
+        if self.fused_update:
+            self._init_fused(learning_rate)
         self.verbose = verbose
         self.reset_nonfinite = reset_nonfinite
         self._nonfinite = torch.zeros((), dtype=torch.int64, device=self.device)
@@ -419,6 +432,59 @@ class PPO:
         self.logger = {}
         self.timing = {"collect_s": 0.0, "gae_s": 0.0, "train_s": 0.0}
         self.history = []   # per iteration: losses, finished-episode mean return, diverged envs
+
+    # --------------------------------------------- fused minibatch step
+    def _init_fused(self, lr):
+        """Flat gradient and Adam state of salp_ppo_mlp (include/salp.h
+        SalpMlpTensor order), the kernels' workspace."""
+        L = _lib.load()
+        pol = self.policy
+        lin = [pol.pi_net[0], pol.pi_net[2], pol.vf_net[0], pol.vf_net[2]]
+        if any(m.out_features != 64 for m in lin) or lin[1].in_features != 64 or lin[0].in_features != self.obs_dim:
+            raise ValueError("salp_ppo_mlp runs the 64-64 tanh MlpPolicy only")
+        self._mlp_tensors = [pol.pi_net[0].weight, pol.pi_net[0].bias, pol.pi_net[2].weight, pol.pi_net[2].bias,
+                             pol.action_net.weight, pol.action_net.bias, pol.log_std,
+                             pol.vf_net[0].weight, pol.vf_net[0].bias, pol.vf_net[2].weight, pol.vf_net[2].bias,
+                             pol.value_net.weight, pol.value_net.bias]
+        for t in self._mlp_tensors:
+            if not (t.is_contiguous() and t.dtype == torch.float32 and t.device == self.device):
+                raise ValueError("policy tensors must be contiguous float32 on the PPO device")
+        P = L.salp_ppo_mlp_num_params(self.obs_dim)
+        z = lambda n: torch.zeros(n, dtype=torch.float32, device=self.device)  # noqa: E731
+        self._f_grads, self._f_m, self._f_v = z(P), z(P), z(P)
+        self._f_step, self._f_gnorm = z(1), z(1)
+        self._f_ws = torch.empty(L.salp_ppo_mlp_workspace_doubles(self.batch_size, self.obs_dim),
+                                 dtype=torch.float64, device=self.device)
+        self._f_lr = float(lr)
+        self._f_adam = _lib.SalpPpoAdam(obs_dim=self.obs_dim, grads=self._f_grads.data_ptr(),
+                                        exp_avg=self._f_m.data_ptr(), exp_avg_sq=self._f_v.data_ptr(),
+                                        step=self._f_step.data_ptr(), grad_norm=self._f_gnorm.data_ptr(),
+                                        lr=self._f_lr, beta1=0.9, beta2=0.999, eps=1e-5,
+                                        max_grad_norm=float(self.max_grad_norm if self.max_grad_norm else 0.0))
+        for i, t in enumerate(self._mlp_tensors):
+            self._f_adam.params[i] = t.data_ptr()
+
+    def _fused_minibatch(self, idx, acc):
+        """One SB3 PPO minibatch step through salp_ppo_mlp: gradient of the
+        loss over rows `idx` (stats added to `acc`), the gradient all-reduce
+        when there are several ranks, then clip_grad_norm_ and Adam."""
+        L = _lib.load()
+        b = self.buf
+        stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        m = _lib.SalpPpoMinibatch(batch=idx.numel(), obs_dim=self.obs_dim,
+                                  normalize_advantage=int(bool(self.normalize_advantage) and idx.numel() > 1),
+                                  idx=idx.data_ptr(), obs=b.obs.data_ptr(), actions=b.actions.data_ptr(),
+                                  old_log_prob=b.log_probs.data_ptr(), advantages=b.advantages.data_ptr(),
+                                  returns=b.returns.data_ptr(), grads=self._f_grads.data_ptr(),
+                                  clip_range=self._clip(), ent_coef=float(self.ent_coef), vf_coef=float(self.vf_coef),
+                                  workspace=self._f_ws.data_ptr(), stats=acc.data_ptr())
+        for i, t in enumerate(self._mlp_tensors):
+            m.params[i] = t.data_ptr()
+        _lib.check(L.salp_ppo_mlp_grads(ctypes.byref(m), stream))
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(self._f_grads)
+            self._f_grads /= dist.get_world_size()
+        _lib.check(L.salp_ppo_mlp_apply(ctypes.byref(self._f_adam), stream))
 
     # ---------------------------------------------------------- rollout
     def collect_rollouts(self):
@@ -532,6 +598,8 @@ class PPO:
     def _minibatch(self, idx, acc):
         """One SB3 PPO gradient step on rollout rows `idx`; adds
         (pg_loss, vf_loss, entropy, clip_fraction) to `acc`."""
+        if self.fused_update:
+            return self._fused_minibatch(idx, acc)
         b, pol = self.buf, self.policy
         N = self.n_steps * self.n_envs
         obs, act = b.obs.reshape(N, -1)[idx], b.actions.reshape(N, -1)[idx]
@@ -563,8 +631,22 @@ class PPO:
     def _graphed_minibatch(self, idx):
         """The same step through a HIP graph: three eager warm-up steps on a
         side stream, then one capture, then replays (static index / stats
-        buffers; Adam is capturable)."""
-        if self._graph is None:
+        buffers; Adam is capturable).  The fused step allocates nothing and
+        reads only persistent buffers: it is captured on its first call and
+        the graph is kept across updates."""
+        if self._graph is not None and self.fused_update and self._g_clip != self._clip():
+            self._graph = None   # a clip_range schedule moved: the captured value is stale
+        if self._graph is None and self.fused_update:
+            if self._graph_warm == 0:
+                self._g_idx = torch.empty_like(idx)
+                self._g_acc = torch.zeros(4, device=self.device)
+            self._g_idx.copy_(idx)
+            self._g_clip = self._clip()
+            self._graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._graph):
+                self._minibatch(self._g_idx, self._g_acc)
+            self._graph_warm = 1
+        elif self._graph is None:
             if self._graph_warm == 0:
                 self._g_idx = torch.empty_like(idx)
                 self._g_acc = torch.zeros(4, device=self.device)
@@ -587,15 +669,15 @@ class PPO:
         self._graph.replay()
 
     def train(self):
-        """n_epochs passes of minibatch updates over the rollout buffer.  The
-        HIP graph of the minibatch step is captured afresh for every update
-        (three warm-up steps, one capture, replays): a graph kept from one
-        update to the next went stale after a collection (from the second or
-        third update on its replays left all-zero, then NaN, gradients while
-        the same minibatch computed eagerly was finite;
-        tools/debug_ppo_drift.py)."""
+        """n_epochs passes of minibatch updates over the rollout buffer.  With
+        the fused step (salp_ppo_mlp) the minibatch graph is captured once and
+        replayed for every update.  With the torch step it is captured afresh
+        for every update (three warm-up steps, one capture, replays): a torch
+        graph kept from one update to the next went stale after a collection
+        (tools/debug_ppo_drift.py)."""
         N = self.n_steps * self.n_envs
-        self._graph, self._graph_warm = None, 0
+        if not self.fused_update:
+            self._graph, self._graph_warm = None, 0
         acc = torch.zeros(4, device=self.device)
         steps = 0
         for _ in range(self.n_epochs):
@@ -605,7 +687,8 @@ class PPO:
                 if self.use_graphs and idx.numel() == self.batch_size:
                     self._graphed_minibatch(idx)
                 else:
-                    self.opt.zero_grad(set_to_none=False)
+                    if not self.fused_update:
+                        self.opt.zero_grad(set_to_none=False)
                     self._minibatch(idx, acc)
                 steps += 1
         if self.use_graphs and self._graph_warm > 0:

@@ -256,6 +256,78 @@ int salp_ppo_loss(int64_t batch, const float* mu, const float* log_std, const fl
                   double clip_range, double ent_coef, double vf_coef, int normalize_advantage,
                   double* workspace, float* out, float* dmu, float* dvalue, void* stream);
 
+/* One PPO minibatch step of the built-in MlpPolicy, fused (stable_baselines3
+ * PPO.train's inner loop for SB3's MlpPolicy with net_arch pi = vf = [64, 64],
+ * tanh: forward, the loss of salp_ppo_loss, backward, clip_grad_norm_, Adam).
+ * The policy's tensors, torch.nn.Linear row-major [out][in], in this order
+ * (obs_dim D <= SALP_OBS_DIM_MAX): */
+enum SalpMlpTensor {
+    SALP_MLP_PI_W1,   /* [64][D] */
+    SALP_MLP_PI_B1,   /* [64]    */
+    SALP_MLP_PI_W2,   /* [64][64] */
+    SALP_MLP_PI_B2,   /* [64]    */
+    SALP_MLP_ACT_W,   /* [3][64] action mean head */
+    SALP_MLP_ACT_B,   /* [3]     */
+    SALP_MLP_LOG_STD, /* [3]     */
+    SALP_MLP_VF_W1,   /* [64][D] */
+    SALP_MLP_VF_B1,   /* [64]    */
+    SALP_MLP_VF_W2,   /* [64][64] */
+    SALP_MLP_VF_B2,   /* [64]    */
+    SALP_MLP_VAL_W,   /* [1][64] value head */
+    SALP_MLP_VAL_B,   /* [1]     */
+    SALP_MLP_N_TENSORS
+};
+/* The flat gradient / Adam-state vectors hold the tensors back to back in
+ * that order: salp_ppo_mlp_offset(D, t) floats in, salp_ppo_mlp_num_params(D)
+ * in all. */
+int64_t salp_ppo_mlp_num_params(int obs_dim);
+int64_t salp_ppo_mlp_offset(int obs_dim, int tensor);
+int64_t salp_ppo_mlp_workspace_doubles(int64_t batch, int obs_dim);
+/* Gradient of the loss over rows idx[0..batch) of the rollout buffer
+ * (obs [N][D], actions [N][3], old_log_prob, advantages, returns [N]) into
+ * grads (flat, overwritten); stats [4] += pg_loss, vf_loss, entropy,
+ * clip_fraction.  Deterministic (no atomics), float32 rows, fp64 sums. */
+typedef struct SalpPpoMinibatch {
+    int64_t batch;
+    int32_t obs_dim;
+    int32_t normalize_advantage;
+    const int64_t* idx;
+    const float* obs;
+    const float* actions;
+    const float* old_log_prob;
+    const float* advantages;
+    const float* returns;
+    float* params[SALP_MLP_N_TENSORS];
+    float* grads;
+    double clip_range;
+    double ent_coef;
+    double vf_coef;
+    double* workspace;     /* salp_ppo_mlp_workspace_doubles(batch, obs_dim) */
+    float* stats;          /* [4] accumulated, or NULL */
+} SalpPpoMinibatch;
+int salp_ppo_mlp_grads(const SalpPpoMinibatch* m, void* stream);
+/* clip_grad_norm_(max_grad_norm; <= 0: no clipping) of the flat gradient,
+ * then torch.optim.Adam (no weight decay / amsgrad) on the tensors; exp_avg
+ * and exp_avg_sq are flat like grads, step [1] is Adam's step count (float32,
+ * incremented here), grad_norm [1] (or NULL) receives the pre-clip norm.  A
+ * multi-GPU learner all-reduces grads between the two calls. */
+typedef struct SalpPpoAdam {
+    int32_t obs_dim;
+    int32_t reserved;
+    float* params[SALP_MLP_N_TENSORS];
+    const float* grads;
+    float* exp_avg;
+    float* exp_avg_sq;
+    float* step;
+    float* grad_norm;
+    double lr;
+    double beta1;
+    double beta2;
+    double eps;
+    double max_grad_norm;
+} SalpPpoAdam;
+int salp_ppo_mlp_apply(const SalpPpoAdam* a, void* stream);
+
 /* ------------------------------------------------ Robot / Nozzle level */
 /* The reference's Robot API for callers that drive the robot directly,
  * without the task env (src/compare_trajectories.py:120-168,

@@ -68,6 +68,7 @@ def _header_struct_fields(name):
         decl = decl.strip()
         if not decl:
             continue
+        decl = re.sub(r"\[[^\]]*\]", "", decl)   # array fields: their name
         first, *rest = decl.split(",")
         fields.append(re.findall(r"(\w+)\s*$", first.strip())[0])
         fields += [r.strip().lstrip("*").strip() for r in rest]
@@ -76,7 +77,8 @@ def _header_struct_fields(name):
 
 @pytest.mark.parametrize("name,cls", [("SalpParams", _abi.SalpParams), ("SalpRolloutBuffers", _lib.SalpRolloutBuffers),
                                       ("SalpTraceBuffer", _lib.SalpTraceBuffer),
-                                      ("SalpPolicyRollout", _lib.SalpPolicyRollout)])
+                                      ("SalpPolicyRollout", _lib.SalpPolicyRollout),
+                                      ("SalpPpoMinibatch", _lib.SalpPpoMinibatch), ("SalpPpoAdam", _lib.SalpPpoAdam)])
 def test_struct_layouts_match_header(name, cls):
     """The ctypes mirrors declare the header's fields in the header's order."""
     assert _header_struct_fields(name) == [f for f, _ in cls._fields_]
@@ -103,3 +105,17 @@ def test_policy_layout_matches_header(tmp_path):
     want = [_abi.POLICY_OFFSETS[n.lower()][0] for n in names[:-1]] + [_abi.POLICY_SIZE]
     assert got == want
     assert _abi.POLICY_OFFSETS["pi_w1"][1] == _abi.POLICY_HIDDEN * _abi.OBS_DIM_MAX
+
+
+def test_fused_ppo_step_layout(lib):
+    """salp_ppo_mlp_*: the flat gradient holds the 13 policy tensors of
+    include/salp.h SalpMlpTensor back to back (torch Linear shapes)."""
+    for d in (6, 10, 14):
+        sizes = [64 * d, 64, 64 * 64, 64, 3 * 64, 3, 3, 64 * d, 64, 64 * 64, 64, 64, 1]
+        offs = [lib.salp_ppo_mlp_offset(d, t) for t in range(14)]
+        assert offs == [sum(sizes[:t]) for t in range(14)]
+        assert lib.salp_ppo_mlp_num_params(d) == sum(sizes)
+        assert lib.salp_ppo_mlp_workspace_doubles(32768, d) > 0
+    assert _lib.N_MLP_TENSORS == len(sizes)
+    assert lib.salp_ppo_mlp_num_params(15) == -1 and lib.salp_ppo_mlp_offset(10, 14) == -1
+    assert lib.salp_ppo_mlp_grads(None, None) == -1

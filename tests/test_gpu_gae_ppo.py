@@ -113,8 +113,12 @@ def test_fused_and_unfused_train_agree_on_the_same_buffer():
     from grasp_lab_salp_amd.ppo import PPO
     from grasp_lab_salp_amd.vec_env import SalpVecEnv
     env = SalpVecEnv(256, seed=4, infos=False)
-    a = PPO("MlpPolicy", env, n_steps=4, batch_size=256, n_epochs=2, seed=2, use_graphs=False, fused_loss=True)
-    b = PPO("MlpPolicy", env, n_steps=4, batch_size=256, n_epochs=2, seed=2, use_graphs=False, fused_loss=False)
+    # the torch update path with either loss head (the fused whole-step kernels
+    # are checked against this path in tests/test_gpu_ppo_mlp.py)
+    a = PPO("MlpPolicy", env, n_steps=4, batch_size=256, n_epochs=2, seed=2, use_graphs=False, fused_loss=True,
+            fused_update=False)
+    b = PPO("MlpPolicy", env, n_steps=4, batch_size=256, n_epochs=2, seed=2, use_graphs=False, fused_loss=False,
+            fused_update=False)
     b.policy.load_state_dict(a.policy.state_dict())
     # plain SGD on both: Adam's per-parameter normalisation would turn float32
     # noise in near-zero gradients into +-lr steps and hide the comparison
@@ -241,7 +245,8 @@ def test_graphed_update_matches_eager_after_several_collections():
     from grasp_lab_salp_amd.ppo import PPO
     from grasp_lab_salp_amd.vec_env import SalpVecEnv
     env = SalpVecEnv(32768, seed=0, infos=False)
-    model = PPO("MlpPolicy", env, n_steps=8, batch_size=32768, n_epochs=2, seed=0, use_graphs=True)
+    model = PPO("MlpPolicy", env, n_steps=8, batch_size=32768, n_epochs=2, seed=0, use_graphs=True,
+                fused_update=False)   # the torch path (the fused step: tests/test_gpu_ppo_mlp.py)
     seen = []
     inner = model._graphed_minibatch
 

@@ -1,0 +1,182 @@
+"""The fused PPO minibatch step (salp_ppo_mlp_grads / salp_ppo_mlp_apply,
+csrc/salp_ppo_mlp.hip) against the torch path it replaces (ppo.PPO with
+fused_update=False: autograd through the ActorCritic and
+torch_ppo_loss, clip_grad_norm_, torch.optim.Adam) — SB3 PPO.train's
+minibatch step for its MlpPolicy (stable-baselines3 >= 2.0; the learner of
+src/train_robot_recurrent_ppo.py:85-107).  Float32 row math with fp64 sums in
+a different order than hipBLASLt: agreement at float32 rounding, stated per
+check."""
+import numpy as np
+import pytest
+import torch
+
+from grasp_lab_salp_amd.ppo import PPO, torch_ppo_loss
+from grasp_lab_salp_amd.vec_env import SalpVecEnv
+
+pytestmark = pytest.mark.gpu
+
+N_ENVS, N_STEPS = 256, 32   # rollout buffer of 8 192 rows
+
+
+def _model(fused, seed=0, batch=4096, **kw):
+    env = SalpVecEnv(N_ENVS, seed=0, infos=False)
+    m = PPO("MlpPolicy", env, n_steps=N_STEPS, batch_size=batch, n_epochs=1, seed=seed, use_graphs=False,
+            fused_update=fused, fused_loss=False, **kw)
+    return m
+
+
+def _fill(m, seed=1):
+    """Random rollout rows and log-probs near the policy's own."""
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    b = m.buf
+    b.obs.copy_(torch.randn(b.obs.shape, generator=g, device="cuda"))
+    b.actions.copy_(torch.randn(b.actions.shape, generator=g, device="cuda") * 0.7)
+    with torch.no_grad():
+        flat = b.obs.reshape(-1, b.obs.shape[-1])
+        lp = m.policy.dist(flat).log_prob(b.actions.reshape(-1, 3)).sum(-1)
+    b.log_probs.copy_((lp + 0.2 * torch.randn(lp.shape, generator=g, device="cuda")).reshape(b.log_probs.shape))
+    b.advantages.copy_(torch.randn(b.advantages.shape, generator=g, device="cuda") * 3 + 0.5)
+    b.returns.copy_(torch.randn(b.returns.shape, generator=g, device="cuda") * 5)
+
+
+def _twins(**kw):
+    a, t = _model(True, **kw), _model(False, **kw)
+    with torch.no_grad():
+        for pa, pt in zip(a.policy.parameters(), t.policy.parameters()):
+            pa.add_(torch.randn_like(pa) * 0.05)
+            pt.copy_(pa)
+    _fill(a)
+    for k in ("obs", "actions", "log_probs", "advantages", "returns"):
+        getattr(t.buf, k).copy_(getattr(a.buf, k))
+    return a, t
+
+
+def _torch_grads(t, idx, norm=True):
+    """The torch path's gradient (before clipping) and loss statistics."""
+    b, pol = t.buf, t.policy
+    N = t.n_steps * t.n_envs
+    obs, act = b.obs.reshape(N, -1)[idx], b.actions.reshape(N, -1)[idx]
+    pol.zero_grad(set_to_none=True)
+    loss, stats = torch_ppo_loss(pol.action_net(pol.pi_net(obs)), pol.log_std, pol.value(obs), act,
+                                 b.log_probs.reshape(N)[idx], b.advantages.reshape(N)[idx], b.returns.reshape(N)[idx],
+                                 0.2, t.ent_coef, t.vf_coef, norm and idx.numel() > 1)
+    loss.backward()
+    return [p.grad.clone() for p in t._mlp_order()], stats
+
+
+def _fused_grads(a, idx, norm=True):
+    acc = torch.zeros(4, device="cuda")
+    a.normalize_advantage = norm
+    import ctypes
+    from grasp_lab_salp_amd import _lib
+    L = _lib.load()
+    b = a.buf
+    m = _lib.SalpPpoMinibatch(batch=idx.numel(), obs_dim=a.obs_dim, normalize_advantage=int(norm and idx.numel() > 1),
+                              idx=idx.data_ptr(), obs=b.obs.data_ptr(), actions=b.actions.data_ptr(),
+                              old_log_prob=b.log_probs.data_ptr(), advantages=b.advantages.data_ptr(),
+                              returns=b.returns.data_ptr(), grads=a._f_grads.data_ptr(), clip_range=0.2,
+                              ent_coef=float(a.ent_coef), vf_coef=float(a.vf_coef), workspace=a._f_ws.data_ptr(),
+                              stats=acc.data_ptr())
+    for i, t in enumerate(a._mlp_tensors):
+        m.params[i] = t.data_ptr()
+    _lib.check(L.salp_ppo_mlp_grads(ctypes.byref(m), None))
+    torch.cuda.synchronize()
+    P = a._f_grads
+    offs = [L.salp_ppo_mlp_offset(a.obs_dim, t) for t in range(14)]
+    return [P[offs[i]:offs[i + 1]].view_as(t).clone() for i, t in enumerate(a._mlp_tensors)], acc
+
+
+def _close(x, y, rtol):
+    scale = float(y.abs().max()) + 1e-12
+    return float((x - y).abs().max()) <= rtol * scale
+
+
+@pytest.mark.parametrize("batch,norm", [(4096, True), (4096, False), (1000, True), (64, True), (1, True)])
+def test_fused_gradient_equals_torch_autograd(batch, norm):
+    """Every one of the 13 tensors' gradients within 1e-4 of its largest entry
+    (float32 sums of 4 096 products in another order), the statistics within
+    1e-5 relative; ragged batches (1 000 rows, one partial tile) and a batch of
+    one row (no advantage normalisation) included."""
+    a, t = _twins(ent_coef=0.01)
+    t._mlp_order = lambda: [t.policy.pi_net[0].weight, t.policy.pi_net[0].bias, t.policy.pi_net[2].weight,
+                            t.policy.pi_net[2].bias, t.policy.action_net.weight, t.policy.action_net.bias,
+                            t.policy.log_std, t.policy.vf_net[0].weight, t.policy.vf_net[0].bias,
+                            t.policy.vf_net[2].weight, t.policy.vf_net[2].bias, t.policy.value_net.weight,
+                            t.policy.value_net.bias]
+    idx = torch.randperm(N_ENVS * N_STEPS, device="cuda")[:batch]
+    gt, st = _torch_grads(t, idx, norm)
+    gf, sf = _fused_grads(a, idx, norm)
+    names = ["pi_w1", "pi_b1", "pi_w2", "pi_b2", "act_w", "act_b", "log_std", "vf_w1", "vf_b1", "vf_w2", "vf_b2",
+             "val_w", "val_b"]
+    for n, x, y in zip(names, gf, gt):
+        assert x.shape == y.shape, n
+        assert _close(x, y, 1e-4), (n, float((x - y).abs().max()), float(y.abs().max()))
+    for k in range(4):
+        assert abs(float(sf[k]) - float(st[k])) <= 1e-5 * max(1.0, abs(float(st[k]))), (k, sf.tolist(), st.tolist())
+
+
+def test_fused_step_equals_torch_clip_and_adam():
+    """Three minibatch steps (gradient, clip_grad_norm_(0.5), Adam with eps 1e-5)
+    through PPO._minibatch on both paths from the same parameters: parameters
+    within float32 rounding of torch's after every step."""
+    a, t = _twins()
+    acc_a, acc_t = torch.zeros(4, device="cuda"), torch.zeros(4, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(3)
+    for step in range(3):
+        idx = torch.randperm(N_ENVS * N_STEPS, device="cuda", generator=g)[:4096]
+        a._minibatch(idx, acc_a)
+        t.opt.zero_grad(set_to_none=False)
+        t._minibatch(idx, acc_t)
+        torch.cuda.synchronize()
+        for (n, pa), pt in zip(a.policy.named_parameters(), t.policy.parameters()):
+            # Adam moves every entry by up to lr = 3e-4 per step; the float32
+            # rounding of the gradient moves that step by far less (most by
+            # < 1e-7; an entry whose gradient is near Adam's eps 1e-5, where
+            # g / (|g| + eps) is steepest, by at most a few 1e-6)
+            d = (pa - pt).detach().abs()
+            assert float(d.max()) <= 1e-5, (step, n, float(d.max()))
+            assert float((d > 1e-7).float().mean()) <= 0.01, (step, n)
+    assert float(a._f_step) == 3.0
+    assert torch.allclose(acc_a, acc_t, rtol=1e-4, atol=1e-6)
+
+
+def test_fused_graph_is_kept_and_equals_eager():
+    """PPO with the fused step replays one graph captured in the first update
+    for every later update; in the third update a replay equals the same
+    minibatch run eagerly from the same state, bit for bit (no atomics), and
+    everything stays finite."""
+    env = SalpVecEnv(32768, seed=0, infos=False)
+    model = PPO("MlpPolicy", env, n_steps=8, batch_size=32768, n_epochs=2, seed=0, use_graphs=True)
+    assert model.fused_update
+    seen, graphs = [], []
+    inner = model._graphed_minibatch
+
+    def state():
+        return [t.detach().clone() for t in model._mlp_tensors] + [model._f_m.clone(), model._f_v.clone(),
+                                                          model._f_step.clone()]
+
+    def put(vals):
+        with torch.no_grad():
+            for d, v in zip(model._mlp_tensors + [model._f_m, model._f_v, model._f_step], vals):
+                d.copy_(v)
+
+    def check(idx):
+        graphs.append(id(model._graph))
+        if model._graph is None or len(model.history) < 2 or seen:
+            return inner(idx)
+        pre = state()
+        inner(idx)
+        post = state()
+        put(pre)
+        model._fused_minibatch(model._g_idx, torch.zeros(4, device="cuda"))
+        eager = state()
+        seen.append(all(torch.equal(x, y) for x, y in zip(post, eager)))
+        put(post)
+
+    model._graphed_minibatch = check
+    model.learn(3 * 8 * 32768)
+    assert seen and seen[0]
+    assert len(set(graphs[1:])) == 1, "one graph, kept across updates"
+    assert all(bool(torch.isfinite(p).all()) for p in model.policy.parameters())
+    for row in model.history:
+        assert np.isfinite(row["vf_loss"]) and np.isfinite(row["pg_loss"])

@@ -172,6 +172,24 @@ static void abi_host_paths(void) {
     CHECK(salp_ppo_loss(0, NULL, NULL, NULL, NULL, NULL, NULL, NULL, 0.2, 0, 0.5, 1, NULL, NULL, NULL, NULL, NULL) ==
           SALP_EINVAL);
     CHECK(salp_math_selftest(NULL, NULL, 1, NULL, NULL) == SALP_EINVAL);
+    /* fused PPO step: layout queries and argument checks (no GPU) */
+    CHECK(salp_ppo_mlp_num_params(10) == 2 * (64 * 10 + 64 + 64 * 64 + 64) + 3 * 64 + 3 + 3 + 64 + 1);
+    CHECK(salp_ppo_mlp_offset(10, SALP_MLP_N_TENSORS) == salp_ppo_mlp_num_params(10));
+    CHECK(salp_ppo_mlp_num_params(0) == -1 && salp_ppo_mlp_workspace_doubles(0, 10) == -1);
+    CHECK(salp_ppo_mlp_grads(NULL, NULL) == SALP_EINVAL);
+    {
+        SalpPpoMinibatch mb;
+        memset(&mb, 0, sizeof mb);
+        mb.batch = 64;
+        mb.obs_dim = 10;
+        CHECK(salp_ppo_mlp_grads(&mb, NULL) == SALP_EINVAL);   /* null buffers */
+        SalpPpoAdam ad;
+        memset(&ad, 0, sizeof ad);
+        ad.obs_dim = 10;
+        CHECK(salp_ppo_mlp_apply(&ad, NULL) == SALP_EINVAL);
+        ad.obs_dim = 99;
+        CHECK(salp_ppo_mlp_apply(&ad, NULL) == SALP_EINVAL);
+    }
 }
 
 #ifdef SALP_SAN_GPU
