@@ -392,46 +392,87 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
 
 // Flat gradient = sum of the block partials (fp64); d loss / d log_std gets its
 // row sums and - ent_coef; block 0 also adds the loss statistics to stats[4].
-__global__ __launch_bounds__(256) void k_mlp_reduce(SalpPpoMinibatch m, Layout L, int nb, const float* part,
-                                                    const double* stat_part) {
+// One block per 64 parameters: its 16 waves take every 16th partial each (at
+// most 16 independent loads per lane, all in flight at once), then wave 0 adds
+// the 16 wave sums in a fixed order (deterministic).
+constexpr int NT_RED = 1024, RED_G = NT_RED / 64, RED_T = NB_MAX / RED_G;
+__global__ __launch_bounds__(NT_RED) void k_mlp_reduce(SalpPpoMinibatch m, Layout L, int nb, const float* part,
+                                                       const double* stat_part) {
+    __shared__ double sh[RED_G][64];
     const int64_t P = L.off[SALP_MLP_N_TENSORS];
-    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int l = threadIdx.x % 64, g = threadIdx.x / 64;
+    const int64_t p = (int64_t)blockIdx.x * 64 + l;
     const int64_t ols = L.off[SALP_MLP_LOG_STD];
+    const bool is_ls = p >= ols && p < ols + NA;
+    double s = 0.0;
     if (p < P) {
-        double s = 0.0;
-        if (p >= ols && p < ols + NA) {
-            for (int b = 0; b < nb; ++b) s += stat_part[(int64_t)b * NSTAT + 3 + (p - ols)];
-            s = (double)((float)s - (float)m.ent_coef);
-        } else {
-            for (int b = 0; b < nb; ++b) s += (double)part[(int64_t)b * P + p];
+        double v[RED_T];
+#pragma unroll
+        for (int t = 0; t < RED_T; ++t) {
+            const int b = g + t * RED_G;
+            v[t] = b >= nb ? 0.0
+                 : is_ls ? stat_part[(int64_t)b * NSTAT + 3 + (p - ols)] : (double)part[(int64_t)b * P + p];
         }
-        m.grads[p] = (float)s;
+#pragma unroll
+        for (int t = 0; t < RED_T; ++t) s += v[t];
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0 && m.stats) {
+    sh[g][l] = s;
+    __syncthreads();
+    if (g == 0 && p < P) {
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < RED_G; ++k) t += sh[k][l];
+        if (is_ls) t = (double)((float)t - (float)m.ent_coef);
+        m.grads[p] = (float)t;
+    }
+    if (blockIdx.x == 0 && g == 1 && m.stats) {
         double t[3] = {0.0, 0.0, 0.0};
-        for (int b = 0; b < nb; ++b)
+        for (int b = l; b < nb; b += 64)
             for (int k = 0; k < 3; ++k) t[k] += stat_part[(int64_t)b * NSTAT + k];
-        const double B = (double)m.batch;
-        float ent = 0.0f;
-        for (int j = 0; j < NA; ++j) ent += 0.5f + kLogSqrt2Pi + m.params[SALP_MLP_LOG_STD][j];
-        m.stats[0] += (float)(-t[0] / B);   // pg_loss
-        m.stats[1] += (float)(t[1] / B);    // vf_loss
-        m.stats[2] += ent;                  // entropy
-        m.stats[3] += (float)(t[2] / B);    // clip fraction
+        for (int o = 32; o > 0; o >>= 1)
+            for (int k = 0; k < 3; ++k) t[k] += __shfl_xor(t[k], o, 64);
+        if (l == 0) {
+            const double B = (double)m.batch;
+            float ent = 0.0f;
+            for (int j = 0; j < NA; ++j) ent += 0.5f + kLogSqrt2Pi + m.params[SALP_MLP_LOG_STD][j];
+            m.stats[0] += (float)(-t[0] / B);   // pg_loss
+            m.stats[1] += (float)(t[1] / B);    // vf_loss
+            m.stats[2] += ent;                  // entropy
+            m.stats[3] += (float)(t[2] / B);    // clip fraction
+        }
     }
 }
 
 // clip_grad_norm_(max_norm) and torch.optim.Adam (no weight decay, no
-// amsgrad), over the flat gradient, in one block.
+// amsgrad), over the flat gradient, in one block: every thread loads its
+// parameters' gradient, moments and weights in one round (AP_MAX each), the
+// block reduces the squared norm, then the thread updates them.
 constexpr int NT_APPLY = 1024;
+constexpr int AP_MAX = 11;   // parameters per thread
+static_assert((int64_t)NT_APPLY * AP_MAX >= 2 * (H * DP + H + H * H + H) + NA * H + 2 * NA + H + 1,
+              "the flat gradient of obs_dim <= 16 fits one apply block");
 __global__ __launch_bounds__(NT_APPLY) void k_mlp_apply(SalpPpoAdam o, Layout L) {
     __shared__ double sh[NT_APPLY / 64];
     __shared__ float s_coef, s_step;
     const int64_t P = L.off[SALP_MLP_N_TENSORS];
+    float g[AP_MAX], m1[AP_MAX], v1[AP_MAX], w1[AP_MAX];
+    float* wp[AP_MAX];
     double q = 0.0;
-    for (int64_t p = threadIdx.x; p < P; p += NT_APPLY) {
-        const double g = o.grads[p];
-        q += g * g;
+#pragma unroll
+    for (int k = 0; k < AP_MAX; ++k) {
+        const int64_t p = threadIdx.x + (int64_t)k * NT_APPLY;
+        wp[k] = nullptr;
+#pragma unroll
+        for (int t = 0; t < SALP_MLP_N_TENSORS; ++t)
+            if (p >= L.off[t] && p < L.off[t + 1]) wp[k] = o.params[t] + (p - L.off[t]);
+        g[k] = m1[k] = v1[k] = w1[k] = 0.0f;
+        if (p < P) {
+            g[k] = o.grads[p];
+            m1[k] = o.exp_avg[p];
+            v1[k] = o.exp_avg_sq[p];
+            w1[k] = *wp[k];
+        }
+        q += (double)g[k] * (double)g[k];
     }
     q = block_sum_d(q, sh, NT_APPLY);
     if (threadIdx.x == 0) {
@@ -450,16 +491,16 @@ __global__ __launch_bounds__(NT_APPLY) void k_mlp_apply(SalpPpoAdam o, Layout L)
     const float b1 = (float)o.beta1, b2 = (float)o.beta2, lr = (float)o.lr, eps = (float)o.eps;
     const float bc1 = 1.0f - powf(b1, step), bc2 = 1.0f - powf(b2, step);
     const float step_size = lr / bc1, bc2_sqrt = sqrtf(bc2);
-    for (int t = 0; t < SALP_MLP_N_TENSORS; ++t) {
-        float* w = o.params[t];
-        for (int64_t i = threadIdx.x; i < L.off[t + 1] - L.off[t]; i += NT_APPLY) {
-            const int64_t p = L.off[t] + i;
-            const float g = o.grads[p] * coef;
-            const float m = b1 * o.exp_avg[p] + (1.0f - b1) * g;
-            const float v = b2 * o.exp_avg_sq[p] + (1.0f - b2) * g * g;
+#pragma unroll
+    for (int k = 0; k < AP_MAX; ++k) {
+        const int64_t p = threadIdx.x + (int64_t)k * NT_APPLY;
+        if (p < P) {
+            const float gc = g[k] * coef;
+            const float m = b1 * m1[k] + (1.0f - b1) * gc;
+            const float v = b2 * v1[k] + (1.0f - b2) * gc * gc;
             o.exp_avg[p] = m;
             o.exp_avg_sq[p] = v;
-            w[i] -= step_size * m / (sqrtf(v) / bc2_sqrt + eps);
+            *wp[k] = w1[k] - step_size * m / (sqrtf(v) / bc2_sqrt + eps);
         }
     }
     if (threadIdx.x == 0) o.step[0] = step;
@@ -501,7 +542,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t salp_ppo_mlp_grads_l
     RowArgs a{m, L, rpb, part, stat_part, adv_part};
     hipLaunchKernelGGL(k_mlp_fwd_bwd, dim3(nb), dim3(NT), 0, s, a);
     const int64_t P = L.off[SALP_MLP_N_TENSORS];
-    hipLaunchKernelGGL(k_mlp_reduce, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, m, L, nb, part, stat_part);
+    hipLaunchKernelGGL(k_mlp_reduce, dim3((unsigned)((P + 63) / 64)), dim3(NT_RED), 0, s, m, L, nb, part, stat_part);
     return hipGetLastError();
 }
 

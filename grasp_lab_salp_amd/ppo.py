@@ -24,8 +24,10 @@ scan (HIP kernel ``salp_gae``) and the policy all stay in HBM:
 * update: for the built-in policy the whole minibatch step (forward, loss,
   backward, clipping, Adam) is four HIP kernels (``salp_ppo_mlp_grads`` /
   ``salp_ppo_mlp_apply``, csrc/salp_ppo_mlp.hip) instead of ~60 torch kernels;
-  on one GPU it is captured into a HIP graph once and replayed per minibatch;
-  other policies take the torch path (autograd, torch Adam, a graph per update).
+  it is captured into a HIP graph once and replayed per minibatch (with
+  several ranks as two graphs around the eager gradient all-reduce); other
+  policies take the torch path (autograd, torch Adam, a graph per update, one
+  GPU only).
 
 The policy is SB3's ``MlpPolicy`` for PPO (separate 64-64 tanh actor and critic,
 orthogonal init, state-independent log-std).  The reference's RecurrentPPO
@@ -370,7 +372,20 @@ class PPO:
         # ... but independent exploration noise per rank (its own env shard)
         self.sample_gen = sampling_generator(seed, self.device)
         multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
-        self.use_graphs = (not multi) if use_graphs is None else bool(use_graphs) and not multi
+        self._multi = multi
+        # the whole minibatch step (forward, loss, backward, clipping, Adam) as
+        # the HIP kernels of salp_ppo_mlp_grads / salp_ppo_mlp_apply for the
+        # built-in policy on a GPU; torch ops + torch Adam otherwise
+        if fused_update and not isinstance(self.policy, ActorCritic):
+            raise ValueError("fused_update=True runs the built-in ActorCritic (64-64 tanh MlpPolicy) only")
+        self.fused_update = (self.device.type == "cuda" and isinstance(self.policy, ActorCritic)
+                             and self.policy.pi_net[0].out_features == 64 if fused_update is None
+                             else bool(fused_update))
+        # HIP graphs: on one rank always; with several ranks for the fused step
+        # only, as two graphs (gradient, then clip + Adam) with the RCCL
+        # all-reduce of the flat gradient between them, outside any capture
+        graphs_ok = not multi or self.fused_update
+        self.use_graphs = graphs_ok if use_graphs is None else bool(use_graphs) and graphs_ok
         # fused Adam on the GPU: one kernel for all parameters instead of ~4
         # elementwise kernels per parameter tensor (capturable either way)
         fused = self.device.type == "cuda"
@@ -379,6 +394,7 @@ class PPO:
         self._graph = None
         self._graph_warm = 0
         self._g_clip = None
+        self._collect_stream = None
         self.n_steps, self.batch_size, self.n_epochs = int(n_steps), int(batch_size), int(n_epochs)
         # clip_range may be an SB3-style schedule: f(progress_remaining) -> value
         self.gamma, self.gae_lambda, self.clip_range = gamma, gae_lambda, clip_range
@@ -389,14 +405,6 @@ class PPO:
         # built-in policy on a GPU; torch ops otherwise (custom policies)
         self.fused_loss = (self.device.type == "cuda" and isinstance(self.policy, ActorCritic)
                            if fused_loss is None else bool(fused_loss))
-        # the whole minibatch step (forward, loss, backward, clipping, Adam) as
-        # the HIP kernels of salp_ppo_mlp_grads / salp_ppo_mlp_apply for the
-        # built-in policy on a GPU; torch ops + torch Adam otherwise
-        if fused_update and not isinstance(self.policy, ActorCritic):
-            raise ValueError("fused_update=True runs the built-in ActorCritic (64-64 tanh MlpPolicy) only")
-        self.fused_update = (self.device.type == "cuda" and isinstance(self.policy, ActorCritic)
-                             and self.policy.pi_net[0].out_features == 64 if fused_update is None
-                             else bool(fused_update))
         if self.fused_update:
             self._init_fused(learning_rate)
         self.verbose = verbose
@@ -464,13 +472,18 @@ class PPO:
         for i, t in enumerate(self._mlp_tensors):
             self._f_adam.params[i] = t.data_ptr()
 
-    def _fused_minibatch(self, idx, acc):
+    def _fused_minibatch(self, idx, acc, part="all"):
         """One SB3 PPO minibatch step through salp_ppo_mlp: gradient of the
         loss over rows `idx` (stats added to `acc`), the gradient all-reduce
-        when there are several ranks, then clip_grad_norm_ and Adam."""
+        when there are several ranks, then clip_grad_norm_ and Adam.  `part`
+        "grads" / "apply" runs only the part before / after the all-reduce
+        (the two graphs of a multi-rank learner)."""
         L = _lib.load()
-        b = self.buf
         stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        if part == "apply":
+            _lib.check(L.salp_ppo_mlp_apply(ctypes.byref(self._f_adam), stream))
+            return
+        b = self.buf
         m = _lib.SalpPpoMinibatch(batch=idx.numel(), obs_dim=self.obs_dim,
                                   normalize_advantage=int(bool(self.normalize_advantage) and idx.numel() > 1),
                                   idx=idx.data_ptr(), obs=b.obs.data_ptr(), actions=b.actions.data_ptr(),
@@ -481,10 +494,16 @@ class PPO:
         for i, t in enumerate(self._mlp_tensors):
             m.params[i] = t.data_ptr()
         _lib.check(L.salp_ppo_mlp_grads(ctypes.byref(m), stream))
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        if part == "grads":
+            return
+        self._allreduce_flat_grads()
+        _lib.check(L.salp_ppo_mlp_apply(ctypes.byref(self._f_adam), stream))
+
+    def _allreduce_flat_grads(self):
+        """Mean of the flat gradient over the ranks (one RCCL message, ~42 KB)."""
+        if self._multi:
             dist.all_reduce(self._f_grads)
             self._f_grads /= dist.get_world_size()
-        _lib.check(L.salp_ppo_mlp_apply(ctypes.byref(self._f_adam), stream))
 
     # ---------------------------------------------------------- rollout
     def collect_rollouts(self):
@@ -643,8 +662,15 @@ class PPO:
             self._g_idx.copy_(idx)
             self._g_clip = self._clip()
             self._graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._graph):
-                self._minibatch(self._g_idx, self._g_acc)
+            if self._multi:   # gradient graph | all-reduce (eager) | clip + Adam graph
+                with torch.cuda.graph(self._graph):
+                    self._fused_minibatch(self._g_idx, self._g_acc, part="grads")
+                self._graph_apply = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self._graph_apply):
+                    self._fused_minibatch(self._g_idx, self._g_acc, part="apply")
+            else:
+                with torch.cuda.graph(self._graph):
+                    self._minibatch(self._g_idx, self._g_acc)
             self._graph_warm = 1
         elif self._graph is None:
             if self._graph_warm == 0:
@@ -667,17 +693,23 @@ class PPO:
         else:
             self._g_idx.copy_(idx)
         self._graph.replay()
+        if self.fused_update and self._multi:
+            self._allreduce_flat_grads()
+            self._graph_apply.replay()
 
     def train(self):
-        """n_epochs passes of minibatch updates over the rollout buffer.  With
-        the fused step (salp_ppo_mlp) the minibatch graph is captured once and
-        replayed for every update.  With the torch step it is captured afresh
-        for every update (three warm-up steps, one capture, replays): a torch
-        graph kept from one update to the next went stale after a collection
-        (tools/debug_ppo_drift.py)."""
+        """n_epochs passes of minibatch updates over the rollout buffer.  The
+        minibatch graph is captured once and replayed for every update.  A
+        torch-step graph (custom policies) kept across updates went stale when
+        eager GEMMs ran on the stream it replays on between updates (the
+        lock-step collection's policy forwards: the captured GEMMs then read a
+        BLAS workspace the eager ones had reused), so learn()
+        runs the collection on a stream of its own; a torch-step graph is
+        still captured afresh per update when the buffer leaves an eager tail
+        minibatch (its GEMMs run on the replay stream)."""
         N = self.n_steps * self.n_envs
-        if not self.fused_update:
-            self._graph, self._graph_warm = None, 0
+        if not self.fused_update and N % self.batch_size:
+            self._graph, self._graph_warm = None, 0   # eager tail minibatch: recapture (see docstring)
         acc = torch.zeros(4, device=self.device)
         steps = 0
         for _ in range(self.n_epochs):
@@ -705,11 +737,22 @@ class PPO:
         it = 0
         start_steps = self.num_timesteps
         stream = torch.cuda.current_stream(self.device)
+        if self._collect_stream is None and self.device.type == "cuda":
+            self._collect_stream = torch.cuda.Stream(self.device)
         while self.num_timesteps < total_timesteps:
             done_frac = (self.num_timesteps - start_steps) / max(total_timesteps - start_steps, 1)
             self._progress = 1.0 - done_frac
             div0 = self._nonfinite.clone()
-            ev = self.collect_rollouts()
+            if self._collect_stream is not None:
+                # eager collection (policy GEMMs) off the stream the update
+                # graph replays on (train() docstring); ordered both ways
+                cs = self._collect_stream
+                cs.wait_stream(stream)
+                with torch.cuda.stream(cs):
+                    ev = self.collect_rollouts()
+                stream.wait_stream(cs)
+            else:
+                ev = self.collect_rollouts()
             self.logger = self.train()
             end = torch.cuda.Event(enable_timing=True)
             end.record(stream)

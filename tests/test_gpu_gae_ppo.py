@@ -238,16 +238,18 @@ def test_collection_is_identical_in_sorted_and_env_order():
 
 
 def test_graphed_update_matches_eager_after_several_collections():
-    """The HIP-graph minibatch step equals the same step run eagerly from the
-    same parameters and Adam state, also in the third update (a graph kept
-    from the first update went stale after collections: zero, then NaN,
-    gradients; tools/debug_ppo_drift.py)."""
+    """The torch-step HIP graph (custom policies), captured in the first
+    update and KEPT, equals the same minibatch run eagerly from the same
+    parameters and Adam state in updates 2-5, with lock-step collections
+    (eager policy GEMMs) in between: n_steps 32 x 10 epochs, the setting in
+    which a kept graph went stale before the collection moved to its own
+    stream (tools/debug_ppo_graph_keep.py, profiles/r3i_torch_graph_keep_sweep.jsonl)."""
     from grasp_lab_salp_amd.ppo import PPO
     from grasp_lab_salp_amd.vec_env import SalpVecEnv
     env = SalpVecEnv(32768, seed=0, infos=False)
-    model = PPO("MlpPolicy", env, n_steps=8, batch_size=32768, n_epochs=2, seed=0, use_graphs=True,
-                fused_update=False)   # the torch path (the fused step: tests/test_gpu_ppo_mlp.py)
-    seen = []
+    model = PPO("MlpPolicy", env, n_steps=32, batch_size=32768, n_epochs=10, seed=0, use_graphs=True,
+                fused_update=False, collect="lockstep")   # the torch path (the fused step: test_gpu_ppo_mlp.py)
+    seen, graphs = {}, set()
     inner = model._graphed_minibatch
 
     def tensors():
@@ -258,8 +260,10 @@ def test_graphed_update_matches_eager_after_several_collections():
         return out
 
     def check(idx):
-        if model._graph is None or len(model.history) < 2 or seen:
+        upd = len(model.history) + 1
+        if model._graph is None or upd < 2 or upd in seen:
             return inner(idx)
+        graphs.add(id(model._graph))
         pre = [t.clone() for t in tensors()]
         inner(idx)
         g_graph = [p.grad.clone() for p in model.policy.parameters()]
@@ -270,15 +274,16 @@ def test_graphed_update_matches_eager_after_several_collections():
         for p in model.policy.parameters():
             p.grad = None
         model._minibatch(model._g_idx, torch.zeros(4, device=model.device))
-        seen.append([torch.equal(a, p.grad) for a, p in zip(g_graph, model.policy.parameters())])
+        seen[upd] = all(torch.equal(a, p.grad) for a, p in zip(g_graph, model.policy.parameters()))
         for p, g in zip(model.policy.parameters(), keep):
             p.grad = g
         for t, s in zip(tensors(), post):
             t.copy_(s)
 
     model._graphed_minibatch = check
-    model.learn(3 * 8 * 32768)
-    assert seen and all(seen[0]), seen
+    model.learn(5 * 32 * 32768)
+    assert sorted(seen) == [2, 3, 4, 5] and all(seen.values()), seen
+    assert len(graphs) == 1, "the graph was recaptured"
     assert all(torch.isfinite(p).all() for p in model.policy.parameters())
     assert all(r["vf_loss"] == r["vf_loss"] for r in model.history)
     env.close()

@@ -1,5 +1,6 @@
-"""Experiment: why does a HIP graph of the PPO minibatch step go stale when it
-is kept across collections?  Runs PPO with the graph KEPT
+"""Experiment: why does a HIP graph of the torch PPO minibatch step (custom
+policies; fused_update=False) go stale when it is kept across collections
+?  Runs PPO with the graph KEPT
 from the first update in several variants and, in the third update, compares
 one graph replay with the same minibatch run eagerly from the same parameters
 and Adam state (bitwise), and reports whether the parameters stay finite.
@@ -65,9 +66,34 @@ class KeptGraphPPO(PPO):
 def run(variant, n_envs, n_steps, updates, collect):
     KeptGraphPPO.variant = variant
     env = SalpVecEnv(n_envs, seed=0, infos=False)
-    m = KeptGraphPPO("MlpPolicy", env, n_steps=n_steps, batch_size=32768, n_epochs=2, seed=0, use_graphs=True,
-                     collect=collect)
-    out = {"variant": variant, "checks": []}
+    if os.environ.get("SPLITK", "1") == "0":   # plain nn.Linear backward (no split-K bmm)
+        from grasp_lab_salp_amd.ppo import SplitKLinear
+        SplitKLinear.ROWS_PER_SPLIT = 1 << 40
+    if os.environ.get("ACT_PATCH") == "nogemm":   # lock-step collection without policy GEMMs
+        from grasp_lab_salp_amd.ppo import ActorCritic
+
+        def act(self, obs, generator=None):
+            n = obs.shape[0]
+            a = 0.5 + 0.1 * torch.randn((n, 3), generator=generator, device=obs.device)
+            z = torch.zeros(n, device=obs.device)
+            return a, z, z.clone()
+        ActorCritic.act = act
+    if os.environ.get("VALUE_PATCH") == "1":   # no value GEMMs outside autograd (collection, bootstrap)
+        from grasp_lab_salp_amd.ppo import ActorCritic
+        real_value = ActorCritic.value
+
+        def value(self, obs):
+            if torch.is_grad_enabled():
+                return real_value(self, obs)
+            return torch.zeros(obs.shape[0], device=obs.device)
+        ActorCritic.value = value
+    m = KeptGraphPPO("MlpPolicy", env, n_steps=n_steps, batch_size=32768,
+                     n_epochs=int(os.environ.get("N_EPOCHS", 2)), seed=0, use_graphs=True, collect=collect,
+                     fused_update=False, fused_loss=os.environ.get("FUSED_LOSS", "1") == "1",
+                     reset_nonfinite=os.environ.get("NO_GUARD") != "1")
+    out = {"variant": variant, "checks": [], "env": {k: os.environ.get(k) for k in
+                                                   ("N_STEPS", "N_EPOCHS", "SPLITK", "FUSED_LOSS", "COLLECT", "ACT_PATCH", "NO_GUARD", "NO_COLLECT", "SYNC_ALLOC", "VALUE_PATCH", "COLLECT_STREAM",
+                                                    "TORCH_BLAS_PREFER_HIPBLASLT")}}
     inner = m._graphed_minibatch
 
     def tensors():
@@ -102,6 +128,39 @@ def run(variant, n_envs, n_steps, updates, collect):
             t.copy_(s)
 
     m._graphed_minibatch = check
+    if os.environ.get("NO_COLLECT") == "1":   # one real collection, then updates on the same buffer
+        real = m.collect_rollouts
+        calls = []
+
+        def collect_once():
+            if not calls:
+                calls.append(1)
+                return real()
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            for e in ev:
+                e.record()
+            return ev
+        m.collect_rollouts = collect_once
+    if os.environ.get("COLLECT_STREAM") == "1":   # eager collection on its own stream
+        real_s = m.collect_rollouts
+        cs = torch.cuda.Stream()
+
+        def collect_on_stream():
+            cs.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(cs):
+                ev = real_s()
+            torch.cuda.current_stream().wait_stream(cs)
+            return ev
+        m.collect_rollouts = collect_on_stream
+    if os.environ.get("SYNC_ALLOC") == "1":   # empty the caching allocator between updates
+        real_c = m.collect_rollouts
+
+        def collect_then_empty():
+            ev = real_c()
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            return ev
+        m.collect_rollouts = collect_then_empty
     m.learn((updates + 1) * n_steps * n_envs)
     out["params_finite"] = all(bool(torch.isfinite(p).all()) for p in m.policy.parameters())
     return out
