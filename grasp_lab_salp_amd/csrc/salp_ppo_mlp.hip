@@ -14,10 +14,10 @@
 //                    rows (the advantage normalisation's mean / std)
 //   k_mlp_fwd_bwd    every block takes a contiguous slice of the minibatch in
 //                    tiles of 64 rows: forward through both networks (weights
-//                    and activations in LDS, 4x4 register tiles), the loss
-//                    head per row, backward to the weight gradients, which
-//                    the block accumulates in registers over its tiles and
-//                    writes as one fp32 partial per parameter
+//                    and activations in LDS, the products on the f32 matrix
+//                    cores), the loss head per row, backward to the weight
+//                    gradients, which the block accumulates in registers over
+//                    its tiles and writes as one fp32 partial per parameter
 //   k_mlp_reduce     sums the partials in fp64 into the flat gradient, and
 //                    the loss statistics
 //   k_mlp_apply      (salp_ppo_mlp_apply) the global gradient norm, the
@@ -110,6 +110,26 @@ __global__ __launch_bounds__(256) void k_mlp_adv_sums(int64_t B, const int64_t* 
     }
 }
 
+// The four GEMM shapes of a 64-row tile run on the f32-input matrix cores
+// (v_mfma_f32_32x32x2_f32 / 16x16x4_f32: exact f32, one fmaf chain in k order
+// per output, the VALU's numerics).  Waves 0-3 take the actor, 4-7 the
+// critic; wave quadrant (qa, qb) owns one 32x32 output tile of every 64x64
+// product.  Lane l supplies A[row l&31][k] and B[k][col l&31] of a step, k
+// from its own half l>>5 of the step's k range (any pairing of k over the
+// steps is a valid sum); results come back with the column on the lane and
+// rows crow(reg, half) in the 16 accumulator registers.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+constexpr int HS2 = H + 4;   // LDS row stride: rows 16-B aligned, rows 8 apart 32 banks apart
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4v mfma16(float a, float b, f32x4v c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+// row of accumulator register r of a 32x32 result, lane half h
+__device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
 __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
     const SalpPpoMinibatch& m = a.m;
     const int D = m.obs_dim;
@@ -118,14 +138,13 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
     // weights (nets: 0 = actor / pi, 1 = critic / vf)
     __shared__ float sW1[2][H][DP];       // [net][unit][input]
     __shared__ float sB1[2][H];
-    __shared__ float sW2T[2][H][H];       // [net][input k][unit j]   (forward)
-    __shared__ float sW2[2][H][H];        // [net][unit j][input k]   (dh1 = W2^T dz2)
+    __shared__ __attribute__((aligned(16))) float sW2[2][H][HS2];   // [net][unit j][input k]
     __shared__ float sB2[2][H];
     __shared__ float sAw[NA][H], sAb[NA], sLs[NA], sVw[H], sVb;
     // one tile of rows
     __shared__ float sX[TR][DP];
-    __shared__ float sH1[2][TR][HS];      // h1, then dz1 in place
-    __shared__ float sH2[2][TR][HS];      // h2, then dz2 in place
+    __shared__ __attribute__((aligned(16))) float sH1[2][TR][HS2];  // h1, then dz1 in place
+    __shared__ __attribute__((aligned(16))) float sH2[2][TR][HS2];  // h2, then dz2 in place
     __shared__ float sDmu[TR][NA], sDv[TR];
     __shared__ float sNorm[2];
     __shared__ double sRed[NT / 64];
@@ -137,9 +156,7 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
     }
     for (int e = tid; e < 2 * H * H; e += NT) {
         const int net = e / (H * H), j = (e / H) % H, k = e % H;
-        const float w = m.params[net ? SALP_MLP_VF_W2 : SALP_MLP_PI_W2][j * H + k];
-        sW2T[net][k][j] = w;
-        sW2[net][j][k] = w;
+        sW2[net][j][k] = m.params[net ? SALP_MLP_VF_W2 : SALP_MLP_PI_W2][j * H + k];
     }
     for (int e = tid; e < 2 * H; e += NT) {
         const int net = e / H, j = e % H;
@@ -168,13 +185,13 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
     }
     __syncthreads();
 
-    // GEMM thread mapping: half the block per network, 16 x 16 groups of 4 x 4
-    const int net = tid / 256, tt = tid % 256, g4a = (tt / 16) * 4, g4b = (tt % 16) * 4;
+    const int w = tid / 64, l = tid % 64, net = w >> 2, q = w & 3, qa = q >> 1, qb = q & 1;
+    const int lc = l & 31, lh = l >> 5;
     // gradient accumulators, kept over the block's tiles
-    float gW2[4][4] = {};      // dW2[net][g4a + i][g4b + c]   (unit j, input k)
-    float gB2[4] = {};         // db2[net][g4a + i]            (threads with g4b == 0)
-    float gW1[4] = {};         // dW1 entries e = tid + q * NT of the [2][H][DP] layout
-    float gB1 = 0.0f;          // db1[tid / H][tid % H]          (threads < 2 H)
+    f32x16 gW2 = {};           // dW2[net][32 qa + crow(r, lh)][32 qb + lc]
+    f32x4v gW1 = {};           // dW1[net][16 q + 4 (l >> 4) + r][l & 15]
+    float gB1 = 0.0f;          // db1[tid / H][tid % H]           (tid < 2 H)
+    float gB2 = 0.0f;          // db2[(tid - 2H) / H][tid % H]     (2 H <= tid < 4 H)
     float gHead = 0.0f;        // dWa (tid < 192), dVw (192 <= tid < 256)
     float gHeadB = 0.0f;       // dab (256 <= tid < 259), dvb (tid == 259)
     double st[NSTAT] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
@@ -197,48 +214,42 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
             sX[r][k] = (r < nrows && k < D) ? m.obs[m.idx[row0 + r] * D + k] : 0.0f;
         }
         __syncthreads();
-        // ---- layer 1: h1 = tanh(W1 x + b1)
+        // ---- layer 1: h1 = tanh(x W1^T + b1)     (K = 16: 8 steps)
         {
-            float acc[4][4];
-            for (int i = 0; i < 4; ++i)
-                for (int c = 0; c < 4; ++c) acc[i][c] = sB1[net][g4b + c];
-            for (int k = 0; k < D; ++k) {
-                float x[4], w[4];
-                for (int i = 0; i < 4; ++i) x[i] = sX[g4a + i][k];
-                for (int c = 0; c < 4; ++c) w[c] = sW1[net][g4b + c][k];
-                for (int i = 0; i < 4; ++i)
-                    for (int c = 0; c < 4; ++c) acc[i][c] = fmaf(x[i], w[c], acc[i][c]);
+            const float b = sB1[net][32 * qb + lc];
+            f32x16 acc = {b, b, b, b, b, b, b, b, b, b, b, b, b, b, b, b};
+#pragma unroll
+            for (int s = 0; s < DP / 2; ++s) {
+                const int k = (DP / 2) * lh + s;
+                acc = mfma32(sX[32 * qa + lc][k], sW1[net][32 * qb + lc][k], acc);
             }
-            for (int i = 0; i < 4; ++i)
-                for (int c = 0; c < 4; ++c) sH1[net][g4a + i][g4b + c] = tanhf(acc[i][c]);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sH1[net][32 * qa + crow(r, lh)][32 * qb + lc] = tanhf(acc[r]);
         }
         __syncthreads();
-        // ---- layer 2: h2 = tanh(W2 h1 + b2)
+        // ---- layer 2: h2 = tanh(h1 W2^T + b2)    (K = 64: 32 steps, k = 32 half + 4 s4 + e)
         {
-            float acc[4][4];
-            for (int i = 0; i < 4; ++i)
-                for (int c = 0; c < 4; ++c) acc[i][c] = sB2[net][g4b + c];
-            for (int k = 0; k < H; ++k) {
-                float x[4];
-                for (int i = 0; i < 4; ++i) x[i] = sH1[net][g4a + i][k];
-                const float4 w = *reinterpret_cast<const float4*>(&sW2T[net][k][g4b]);
-                for (int i = 0; i < 4; ++i) {
-                    acc[i][0] = fmaf(x[i], w.x, acc[i][0]);
-                    acc[i][1] = fmaf(x[i], w.y, acc[i][1]);
-                    acc[i][2] = fmaf(x[i], w.z, acc[i][2]);
-                    acc[i][3] = fmaf(x[i], w.w, acc[i][3]);
-                }
+            const float b = sB2[net][32 * qb + lc];
+            f32x16 acc = {b, b, b, b, b, b, b, b, b, b, b, b, b, b, b, b};
+#pragma unroll
+            for (int s4 = 0; s4 < 8; ++s4) {
+                const float4 x = *reinterpret_cast<const float4*>(&sH1[net][32 * qa + lc][32 * lh + 4 * s4]);
+                const float4 y = *reinterpret_cast<const float4*>(&sW2[net][32 * qb + lc][32 * lh + 4 * s4]);
+                acc = mfma32(x.x, y.x, acc);
+                acc = mfma32(x.y, y.y, acc);
+                acc = mfma32(x.z, y.z, acc);
+                acc = mfma32(x.w, y.w, acc);
             }
-            for (int i = 0; i < 4; ++i)
-                for (int c = 0; c < 4; ++c) sH2[net][g4a + i][g4b + c] = tanhf(acc[i][c]);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sH2[net][32 * qa + crow(r, lh)][32 * qb + lc] = tanhf(acc[r]);
         }
         __syncthreads();
         // ---- heads and the loss head: 8 threads per row
         {
             const int r = tid / 8, p = tid % 8;
             float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-            for (int q = 0; q < 8; ++q) {
-                const int j = p * 8 + q;
+            for (int qq = 0; qq < 8; ++qq) {
+                const int j = p * 8 + qq;
                 const float hp = sH2[0][r][j], hv = sH2[1][r][j];
                 s[0] = fmaf(hp, sAw[0][j], s[0]);
                 s[1] = fmaf(hp, sAw[1][j], s[1]);
@@ -310,49 +321,47 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
             sH2[n][r][j] = dh * (1.0f - h * h);
         }
         __syncthreads();
-        // ---- dW2 += dz2^T h1, db2 += sum dz2 (4x4 tile: units g4a.., inputs g4b..)
-        for (int r = 0; r < TR; ++r) {
-            float z[4], x[4];
-            for (int i = 0; i < 4; ++i) z[i] = sH2[net][r][g4a + i];
-            for (int c = 0; c < 4; ++c) x[c] = sH1[net][r][g4b + c];
-            for (int i = 0; i < 4; ++i)
-                for (int c = 0; c < 4; ++c) gW2[i][c] = fmaf(z[i], x[c], gW2[i][c]);
-            if (g4b == 0)
-                for (int i = 0; i < 4; ++i) gB2[i] += z[i];
-        }
-        __syncthreads();
-        // ---- dh1 = W2^T dz2, dz1 = dh1 (1 - h1^2) in place (rows g4a.., inputs g4b..)
+        // ---- dW2 += dz2^T h1 (K = rows: r = 16 (s / 8) + 8 half + s % 8), db2 += sum dz2,
+        //      dh1 = dz2 W2 (K = units: 32 half + 4 s4 + e), dz1 = dh1 (1 - h1^2)
+        float dz1[16];
         {
-            float acc[4][4] = {};
-            for (int j = 0; j < H; ++j) {
-                float z[4];
-                for (int i = 0; i < 4; ++i) z[i] = sH2[net][g4a + i][j];
-                const float4 w = *reinterpret_cast<const float4*>(&sW2[net][j][g4b]);
-                for (int i = 0; i < 4; ++i) {
-                    acc[i][0] = fmaf(z[i], w.x, acc[i][0]);
-                    acc[i][1] = fmaf(z[i], w.y, acc[i][1]);
-                    acc[i][2] = fmaf(z[i], w.z, acc[i][2]);
-                    acc[i][3] = fmaf(z[i], w.w, acc[i][3]);
-                }
+#pragma unroll
+            for (int s = 0; s < 32; ++s) {
+                const int r = 16 * (s >> 3) + 8 * lh + (s & 7);
+                gW2 = mfma32(sH2[net][r][32 * qa + lc], sH1[net][r][32 * qb + lc], gW2);
             }
-            // only this thread's own h1 entries are read and replaced here (the
-            // dW2 pass that read every h1 ended at the barrier above)
-            for (int i = 0; i < 4; ++i)
-                for (int c = 0; c < 4; ++c) {
-                    const float h = sH1[net][g4a + i][g4b + c];
-                    sH1[net][g4a + i][g4b + c] = acc[i][c] * (1.0f - h * h);
-                }
-        }
-        __syncthreads();
-        // ---- dW1 += dz1^T x, db1 += sum dz1
-        for (int q = 0; q < (2 * H * DP) / NT; ++q) {
-            const int e = tid + q * NT;
-            const int n = e / (H * DP), u = (e / DP) % H, k = e % DP;
-            if (k < D) {
+            f32x16 dh = {};
+#pragma unroll
+            for (int s4 = 0; s4 < 8; ++s4) {
+                const float4 z = *reinterpret_cast<const float4*>(&sH2[net][32 * qa + lc][32 * lh + 4 * s4]);
+                const int j = 32 * lh + 4 * s4;
+                dh = mfma32(z.x, sW2[net][j + 0][32 * qb + lc], dh);
+                dh = mfma32(z.y, sW2[net][j + 1][32 * qb + lc], dh);
+                dh = mfma32(z.z, sW2[net][j + 2][32 * qb + lc], dh);
+                dh = mfma32(z.w, sW2[net][j + 3][32 * qb + lc], dh);
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float h = sH1[net][32 * qa + crow(r, lh)][32 * qb + lc];
+                dz1[r] = dh[r] * (1.0f - h * h);
+            }
+            if (tid >= 2 * H && tid < 4 * H) {
+                const int n = (tid - 2 * H) / H, j = tid % H;
                 float acc = 0.0f;
-                for (int r = 0; r < TR; ++r) acc = fmaf(sH1[n][r][u], sX[r][k], acc);
-                gW1[q] += acc;
+                for (int r = 0; r < TR; ++r) acc += sH2[n][r][j];
+                gB2 += acc;
             }
+        }
+        __syncthreads();   // every read of h1 is done: dz1 replaces it
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sH1[net][32 * qa + crow(r, lh)][32 * qb + lc] = dz1[r];
+        __syncthreads();
+        // ---- dW1 += dz1^T x (16x16x4: wave q takes units 16 q .. 16 q + 15; r = 16 (l >> 4) + s),
+        //      db1 += sum dz1
+#pragma unroll
+        for (int s = 0; s < TR / 4; ++s) {
+            const int r = 16 * (l >> 4) + s;
+            gW1 = mfma16(sH1[net][r][16 * q + (l & 15)], sX[r][l & 15], gW1);
         }
         if (tid < 2 * H) {
             const int n = tid / H, u = tid % H;
@@ -367,19 +376,15 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
     float* P = a.part + (int64_t)blockIdx.x * a.L.off[SALP_MLP_N_TENSORS];
     {
         const int64_t ow2 = a.L.off[net ? SALP_MLP_VF_W2 : SALP_MLP_PI_W2];
-        for (int i = 0; i < 4; ++i)
-            for (int c = 0; c < 4; ++c) P[ow2 + (g4a + i) * H + g4b + c] = gW2[i][c];
-        if (g4b == 0) {
-            const int64_t ob2 = a.L.off[net ? SALP_MLP_VF_B2 : SALP_MLP_PI_B2];
-            for (int i = 0; i < 4; ++i) P[ob2 + g4a + i] = gB2[i];
-        }
-    }
-    for (int q = 0; q < (2 * H * DP) / NT; ++q) {
-        const int e = tid + q * NT;
-        const int n = e / (H * DP), u = (e / DP) % H, k = e % DP;
-        if (k < D) P[a.L.off[n ? SALP_MLP_VF_W1 : SALP_MLP_PI_W1] + u * D + k] = gW1[q];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) P[ow2 + (32 * qa + crow(r, lh)) * H + 32 * qb + lc] = gW2[r];
+        const int64_t ow1 = a.L.off[net ? SALP_MLP_VF_W1 : SALP_MLP_PI_W1];
+        if ((l & 15) < D)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) P[ow1 + (16 * q + 4 * (l >> 4) + r) * D + (l & 15)] = gW1[r];
     }
     if (tid < 2 * H) P[a.L.off[tid / H ? SALP_MLP_VF_B1 : SALP_MLP_PI_B1] + tid % H] = gB1;
+    else if (tid < 4 * H) P[a.L.off[(tid - 2 * H) / H ? SALP_MLP_VF_B2 : SALP_MLP_PI_B2] + tid % H] = gB2;
     if (tid < NA * H) P[a.L.off[SALP_MLP_ACT_W] + tid] = gHead;
     else if (tid < NA * H + H) P[a.L.off[SALP_MLP_VAL_W] + tid - NA * H] = gHead;
     else if (tid < NA * H + H + NA) P[a.L.off[SALP_MLP_ACT_B] + tid - NA * H - H] = gHeadB;
@@ -454,17 +459,26 @@ static_assert((int64_t)NT_APPLY * AP_MAX >= 2 * (H * DP + H + H * H + H) + NA * 
 __global__ __launch_bounds__(NT_APPLY) void k_mlp_apply(SalpPpoAdam o, Layout L) {
     __shared__ double sh[NT_APPLY / 64];
     __shared__ float s_coef, s_step;
-    const int64_t P = L.off[SALP_MLP_N_TENSORS];
+    __shared__ float* s_base[SALP_MLP_N_TENSORS];   // params[t] - off[t]: p indexes it directly
+    __shared__ int s_off[SALP_MLP_N_TENSORS];
+#pragma unroll
+    for (int t = 0; t < SALP_MLP_N_TENSORS; ++t)
+        if (threadIdx.x == t) {
+            s_base[t] = o.params[t] - L.off[t];
+            s_off[t] = (int)L.off[t];
+        }
+    const int P = (int)L.off[SALP_MLP_N_TENSORS];
+    __syncthreads();
     float g[AP_MAX], m1[AP_MAX], v1[AP_MAX], w1[AP_MAX];
     float* wp[AP_MAX];
     double q = 0.0;
 #pragma unroll
     for (int k = 0; k < AP_MAX; ++k) {
-        const int64_t p = threadIdx.x + (int64_t)k * NT_APPLY;
-        wp[k] = nullptr;
+        const int p = threadIdx.x + k * NT_APPLY;
+        int t = 0;
 #pragma unroll
-        for (int t = 0; t < SALP_MLP_N_TENSORS; ++t)
-            if (p >= L.off[t] && p < L.off[t + 1]) wp[k] = o.params[t] + (p - L.off[t]);
+        for (int u = 1; u < SALP_MLP_N_TENSORS; ++u) t += p >= s_off[u] ? 1 : 0;
+        wp[k] = s_base[t] + p;
         g[k] = m1[k] = v1[k] = w1[k] = 0.0f;
         if (p < P) {
             g[k] = o.grads[p];
@@ -493,7 +507,7 @@ __global__ __launch_bounds__(NT_APPLY) void k_mlp_apply(SalpPpoAdam o, Layout L)
     const float step_size = lr / bc1, bc2_sqrt = sqrtf(bc2);
 #pragma unroll
     for (int k = 0; k < AP_MAX; ++k) {
-        const int64_t p = threadIdx.x + (int64_t)k * NT_APPLY;
+        const int p = threadIdx.x + k * NT_APPLY;
         if (p < P) {
             const float gc = g[k] * coef;
             const float m = b1 * m1[k] + (1.0f - b1) * gc;
