@@ -510,7 +510,7 @@ class PPO:
         """n_steps lock-step env-steps into the buffer, then GAE.  Returns the
         HIP events (start, before GAE, after GAE) on the current stream, so
         the split of the GPU timeline is attributed to the right phase."""
-        b, sim, pol = self.buf, self.sim, self.policy
+        b, sim = self.buf, self.sim
         stream = torch.cuda.current_stream(self.device)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         ev[0].record(stream)
@@ -521,7 +521,7 @@ class PPO:
             return self._collect_chained(ev, stream)
         for t in range(self.n_steps):
             obs = self._obs
-            a, v, lp = pol.act(obs, generator=self.sample_gen)
+            a, v, lp = self._act(t, obs)
             r = sim.step(torch.clamp(a, self.low, self.high), auto_reset=True, want_terminal_obs=True)
             rew = r.reward.float()
             reached = r.terminated.clone()   # the task's own termination: target reached
@@ -531,7 +531,7 @@ class PPO:
             # no host sync in the loop: the bootstrap value is computed for every
             # env and selected where the episode was truncated, not terminated
             with torch.no_grad():
-                tv = pol.value(r.terminal_obs)
+                tv = self._terminal_value(r.terminal_obs)
             rew = timeout_bootstrap(rew, r.terminated, r.truncated, tv, self.gamma)
             done = (r.terminated | r.truncated)
             ended = done if bad is None else done & ~bad    # episodes that ended by the task's rules
@@ -548,12 +548,25 @@ class PPO:
             self._obs = r.obs
             self._episode_starts = done.float()
         with torch.no_grad():
-            last_values = pol.value(self._obs).contiguous()
+            last_values = self._last_values().contiguous()
         ev[1].record(stream)
         compute_gae(b.rewards, b.values, b.episode_starts, last_values, self._episode_starts.contiguous(),
                     self.gamma, self.gae_lambda, b.advantages, b.returns)
         ev[2].record(stream)
         return ev
+
+    # hooks of the lock-step collection (RecurrentPPO carries LSTM states through them)
+    def _act(self, t, obs):
+        """(action, value, log_prob) of step t's observations."""
+        return self.policy.act(obs, generator=self.sample_gen)
+
+    def _terminal_value(self, terminal_obs):
+        """V(terminal observation) for the timeout bootstrap."""
+        return self.policy.value(terminal_obs)
+
+    def _last_values(self):
+        """V(observation after the last step) for GAE."""
+        return self.policy.value(self._obs)
 
     def _collect_chained(self, ev, stream):
         """collect_rollouts on salp_collect: the same buffers, bootstrap and

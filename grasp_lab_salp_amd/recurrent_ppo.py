@@ -1,0 +1,249 @@
+"""RecurrentPPO with sb3-contrib's ``MlpLstmPolicy`` on the batched simulator:
+the learner of ``/root/reference/src/train_robot_recurrent_ppo.py:85-107``
+(``lstm_hidden_size=256, n_lstm_layers=1, enable_critic_lstm=True,
+shared_lstm=False``; lr 3e-4, n_steps 2048, batch 64, 10 epochs, gamma 0.99,
+GAE lambda 0.95, clip 0.2, ent 0, vf 0.5, max_grad_norm 0.5).
+
+sb3-contrib (>= 2.0) is not installed here: its semantics are restated, and
+parity with it is unpinned.  What is kept:
+
+* policy: an LSTM for the actor and another for the critic on the raw
+  observation, then SB3's ``net_arch`` pi=[64, 64] / vf=[64, 64] tanh MLPs, the
+  action / value heads and a state-independent log-std (orthogonal init of the
+  MLPs and heads as SB3; the LSTMs keep torch's default init, as sb3-contrib);
+* the LSTM states are zeroed where an episode starts, before that step
+  (sb3-contrib ``_process_sequence``), in collection and in training alike;
+* the timeout bootstrap evaluates the terminal observation with the critic
+  state after the step, episode start 0; the last value with the episode
+  starts of the next step (``RecurrentPPO.collect_rollouts``);
+* training re-runs the LSTMs over sequences from the states stored at their
+  first step.  sb3-contrib cuts an env's rollout into sequences at episode
+  starts and pads them; here every env's rollout is cut into fixed
+  ``seq_len``-step sequences (the state stored every ``seq_len`` steps) and
+  episode starts inside a sequence zero the state there.  Both compute the
+  same forward pass per step; minibatches are ``batch_size // seq_len``
+  sequences (no padding rows).
+
+Collection is lock-step (``salp_step`` per env-step: the LSTM policy is not
+evaluated inside the simulation kernel; ``salp_collect`` runs the MLP
+policy), with the same divergence guard, episode statistics and HIP-event
+phase timings as :class:`~grasp_lab_salp_amd.ppo.PPO`.
+"""
+import math
+
+import torch
+from torch import nn
+
+from .ppo import PPO, _ortho, allreduce_gradients
+
+__all__ = ["RecurrentActorCritic", "RecurrentPPO"]
+
+
+class RecurrentActorCritic(nn.Module):
+    """sb3-contrib ``RecurrentActorCriticPolicy`` (MlpLstmPolicy) with separate
+    actor and critic LSTMs.  A recurrent state is one [4, n, H] tensor:
+    (h, c) of the actor LSTM, then (h, c) of the critic LSTM."""
+
+    def __init__(self, obs_dim, act_dim, lstm_hidden_size=256, net_arch=(64, 64)):
+        super().__init__()
+        self.hidden = int(lstm_hidden_size)
+        self.lstm_actor = nn.LSTM(obs_dim, self.hidden)
+        self.lstm_critic = nn.LSTM(obs_dim, self.hidden)
+
+        def mlp():
+            layers, d = [], self.hidden
+            for h in net_arch:
+                layers += [_ortho(nn.Linear(d, h), math.sqrt(2)), nn.Tanh()]
+                d = h
+            return nn.Sequential(*layers), d
+
+        self.pi_net, d_pi = mlp()
+        self.vf_net, d_vf = mlp()
+        self.action_net = _ortho(nn.Linear(d_pi, act_dim), 0.01)
+        self.value_net = _ortho(nn.Linear(d_vf, 1), 1.0)
+        self.log_std = nn.Parameter(torch.zeros(act_dim))
+
+    def initial_state(self, n, device=None):
+        return torch.zeros(4, n, self.hidden, device=device)
+
+    @staticmethod
+    def _run(lstm, x, h, c, starts):
+        """x [T, n, D] through `lstm` (torch's LSTM equations and parameter
+        layout, gates i, f, g, o) from (h, c) [n, H]; the state is zeroed where
+        starts[t] (an episode starts at step t), before step t.  The input
+        projection of all T steps is one GEMM; each step is one GEMM plus
+        elementwise work, all capturable in a HIP graph (a fused RNN library
+        call cannot reset states inside a sequence).
+        Returns (outputs [T, n, H], h, c)."""
+        T, n, D = x.shape
+        gx = torch.addmm(lstm.bias_ih_l0 + lstm.bias_hh_l0, x.reshape(T * n, D),
+                         lstm.weight_ih_l0.t()).view(T, n, -1)
+        w_hh = lstm.weight_hh_l0.t()
+        outs = []
+        for t in range(T):
+            keep = (1.0 - starts[t]).unsqueeze(1)
+            h, c = h * keep, c * keep
+            i, f, g, o = torch.addmm(gx[t], h, w_hh).chunk(4, 1)
+            c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(g)
+            h = torch.sigmoid(o) * torch.tanh(c)
+            outs.append(h)
+        return torch.stack(outs), h, c
+
+    def forward_seq(self, obs, state, starts, critic=True):
+        """Latents of a sequence: obs [T, n, D], state [4, n, H], starts [T, n].
+        Returns (actor latent [T, n, H], critic latent or None, new state)."""
+        lp, hp, cp = self._run(self.lstm_actor, obs, state[0], state[1], starts)
+        if not critic:
+            return lp, None, torch.stack([hp, cp, state[2], state[3]])
+        lv, hv, cv = self._run(self.lstm_critic, obs, state[2], state[3], starts)
+        return lp, lv, torch.stack([hp, cp, hv, cv])
+
+    def _dist(self, latent_pi):
+        mean = self.action_net(self.pi_net(latent_pi))
+        return torch.distributions.Normal(mean, self.log_std.exp().expand_as(mean), validate_args=False)
+
+    def _value(self, latent_vf):
+        return self.value_net(self.vf_net(latent_vf)).squeeze(-1)
+
+    @torch.no_grad()
+    def act(self, obs, state, episode_starts, generator=None):
+        """One step for every env: obs [n, D] -> (action, value, log_prob,
+        new state); the Gaussian noise from `generator` when given."""
+        lp, lv, new = self.forward_seq(obs.unsqueeze(0), state, episode_starts.unsqueeze(0))
+        d = self._dist(lp[0])
+        if generator is None:
+            a = d.sample()
+        else:
+            a = d.mean + d.stddev * torch.randn(d.mean.shape, generator=generator, device=d.mean.device,
+                                                dtype=d.mean.dtype)
+        return a, self._value(lv[0]), d.log_prob(a).sum(-1), new
+
+    @torch.no_grad()
+    def predict_values(self, obs, state, episode_starts):
+        """V(obs) with the critic LSTM from `state` (not advanced)."""
+        lv, _, _ = self._run(self.lstm_critic, obs.unsqueeze(0), state[2], state[3], episode_starts.unsqueeze(0))
+        return self._value(lv[0])
+
+    def evaluate(self, obs, actions, state, starts):
+        """Training pass over sequences: obs [T, n, D], actions [T, n, A],
+        state [4, n, H] at the sequences' first step, starts [T, n].
+        Returns (value, log_prob, entropy), each [T, n]."""
+        lp, lv, _ = self.forward_seq(obs, state, starts)
+        d = self._dist(lp)
+        return self._value(lv), d.log_prob(actions).sum(-1), d.entropy().sum(-1)
+
+
+class RecurrentPPO(PPO):
+    """sb3-contrib ``RecurrentPPO`` on a :class:`~grasp_lab_salp_amd.vec_env.SalpVecEnv`
+    (see the module docstring for the semantics).  ``batch_size`` counts
+    env-steps and must be a multiple of ``seq_len``."""
+
+    def __init__(self, policy, env, learning_rate=3e-4, n_steps=2048, batch_size=64, n_epochs=10, gamma=0.99,
+                 gae_lambda=0.95, clip_range=0.2, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5,
+                 normalize_advantage=True, seed=0, device=None, verbose=0, reset_nonfinite=True,
+                 policy_kwargs=None, seq_len=16, use_graphs=None):
+        sim = getattr(env, "sim", env)
+        kw = dict(policy_kwargs or {})
+        for k, want in (("n_lstm_layers", 1), ("enable_critic_lstm", True), ("shared_lstm", False)):
+            if kw.pop(k, want) != want:
+                raise ValueError(f"policy_kwargs {k}={want} is the supported configuration")
+        if policy == "MlpLstmPolicy":
+            torch.manual_seed(int(seed))
+            policy = RecurrentActorCritic(sim.obs_dim, 3, lstm_hidden_size=kw.pop("lstm_hidden_size", 256),
+                                          net_arch=tuple(kw.pop("net_arch", (64, 64))))
+        elif not isinstance(policy, RecurrentActorCritic):
+            raise ValueError("policy must be 'MlpLstmPolicy' or a RecurrentActorCritic")
+        if kw:
+            raise ValueError(f"unsupported policy_kwargs: {sorted(kw)}")
+        if n_steps % seq_len or batch_size % seq_len:
+            raise ValueError("n_steps and batch_size must be multiples of seq_len")
+        super().__init__(policy, env, learning_rate=learning_rate, n_steps=n_steps, batch_size=batch_size,
+                         n_epochs=n_epochs, gamma=gamma, gae_lambda=gae_lambda, clip_range=clip_range,
+                         ent_coef=ent_coef, vf_coef=vf_coef, max_grad_norm=max_grad_norm,
+                         normalize_advantage=normalize_advantage, seed=seed, device=device, verbose=verbose,
+                         reset_nonfinite=reset_nonfinite, use_graphs=use_graphs, fused_loss=False,
+                         collect="lockstep", fused_update=False)
+        self.seq_len = int(seq_len)
+        self.n_seq = self.n_steps // self.seq_len
+        self._lstm_state = self.policy.initial_state(self.n_envs, self.device)
+        # recurrent state at the first step of every sequence [n_seq, 4, n, H]
+        self.seq_states = torch.zeros(self.n_seq, 4, self.n_envs, self.policy.hidden, device=self.device)
+
+    # -------------------------------------------- collection hooks (PPO)
+    def _act(self, t, obs):
+        if t % self.seq_len == 0:
+            self.seq_states[t // self.seq_len].copy_(self._lstm_state)
+        a, v, lp, self._lstm_state = self.policy.act(obs, self._lstm_state, self._episode_starts,
+                                                     generator=self.sample_gen)
+        return a, v, lp
+
+    def _terminal_value(self, terminal_obs):
+        # the critic state after the step, no reset (the episode ended at it)
+        return self.policy.predict_values(terminal_obs, self._lstm_state, torch.zeros_like(self._episode_starts))
+
+    def _last_values(self):
+        # (a guard reset ends an episode too: the next step's episode start
+        # zeroes that env's state, as for any other episode end)
+        return self.policy.predict_values(self._obs, self._lstm_state, self._episode_starts)
+
+    # ------------------------------------------------------------ update
+    def _seq_minibatch(self, ids, acc):
+        """One PPO gradient step on sequences `ids` (sequence k of env e is
+        id k * n_envs + e)."""
+        b, pol = self.buf, self.policy
+        n, T = self.n_envs, self.seq_len
+        k, e = ids // n, ids % n
+        t = k.unsqueeze(0) * T + torch.arange(T, device=self.device).unsqueeze(1)   # [T, m]
+        ee = e.unsqueeze(0).expand_as(t)
+        obs, act = b.obs[t, ee], b.actions[t, ee]
+        old_lp, adv, ret, starts = b.log_probs[t, ee], b.advantages[t, ee], b.returns[t, ee], b.episode_starts[t, ee]
+        state = self.seq_states[k, :, e].transpose(0, 1)                             # [4, m, H]
+        v, lp, ent = pol.evaluate(obs, act, state, starts)
+        v, lp, ent, old_lp, adv, ret = (x.reshape(-1) for x in (v, lp, ent, old_lp, adv, ret))
+        if self.normalize_advantage and adv.numel() > 1:
+            adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+        ratio = torch.exp(lp - old_lp)
+        cr = self._clip()
+        pg = -torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - cr, 1 + cr)).mean()
+        vf = torch.nn.functional.mse_loss(ret, v)
+        ent_loss = -ent.mean()
+        loss = pg + self.ent_coef * ent_loss + self.vf_coef * vf
+        self.opt.zero_grad(set_to_none=False)
+        loss.backward()
+        allreduce_gradients(list(pol.parameters()))
+        nn.utils.clip_grad_norm_(pol.parameters(), self.max_grad_norm)
+        self.opt.step()
+        clip = ((ratio - 1).abs() > cr).float().mean()
+        acc += torch.stack([pg.detach(), vf.detach(), -ent_loss.detach(), clip.detach()])
+
+    def _minibatch(self, idx, acc):
+        # PPO._graphed_minibatch captures / replays this with `idx` = sequence ids
+        self._seq_minibatch(idx, acc)
+
+    def train(self):
+        """n_epochs passes over the rollout's sequences in random minibatches of
+        batch_size // seq_len sequences.  On one GPU the minibatch step (the
+        BPTT over seq_len steps: ~1 000 small kernels) runs as a HIP graph
+        captured in the first update and kept (PPO._graphed_minibatch; the
+        collection runs on its own stream, PPO.learn); a ragged last
+        minibatch runs eagerly."""
+        total = self.n_seq * self.n_envs
+        per = self.batch_size // self.seq_len
+        if total % per:
+            self._graph, self._graph_warm = None, 0
+        acc = torch.zeros(4, device=self.device)
+        steps = 0
+        for _ in range(self.n_epochs):
+            perm = torch.randperm(total, generator=self.gen, device=self.device)
+            for s in range(0, total, per):
+                ids = perm[s:s + per]
+                if self.use_graphs and ids.numel() == per:
+                    self._graphed_minibatch(ids)
+                else:
+                    self._seq_minibatch(ids, acc)
+                steps += 1
+        if self.use_graphs and self._graph_warm > 0:
+            acc = acc + self._g_acc
+            self._g_acc.zero_()
+        vals = (acc / max(steps, 1)).tolist()
+        return dict(zip(("pg_loss", "vf_loss", "entropy", "clip_frac"), vals))

@@ -1,0 +1,94 @@
+"""The MlpLstmPolicy of RecurrentPPO (grasp_lab_salp_amd/recurrent_ppo.py, the
+learner of /root/reference/src/train_robot_recurrent_ppo.py:85-107; sb3-contrib
+semantics restated, parity with sb3-contrib unpinned): the training pass over
+a stored sequence reproduces what the step-by-step collection computed, and an
+episode start zeroes the recurrent state before its step.  CPU."""
+import pytest
+import torch
+
+from grasp_lab_salp_amd.recurrent_ppo import RecurrentActorCritic, RecurrentPPO
+
+
+def _policy(seed=0, hidden=32):
+    torch.manual_seed(seed)
+    return RecurrentActorCritic(10, 3, lstm_hidden_size=hidden)
+
+
+def test_sequence_pass_equals_stepwise_collection():
+    pol = _policy()
+    T, n = 12, 7
+    g = torch.Generator().manual_seed(1)
+    obs = torch.randn(T, n, 10, generator=g)
+    starts = (torch.rand(T, n, generator=g) < 0.2).float()
+    starts[0] = 1.0
+    state0 = pol.initial_state(n)
+    state = state0
+    acts, vals, lps = [], [], []
+    for t in range(T):
+        a, v, lp, state = pol.act(obs[t], state, starts[t], generator=g)
+        acts.append(a)
+        vals.append(v)
+        lps.append(lp)
+    with torch.no_grad():
+        v, lp, ent = pol.evaluate(obs, torch.stack(acts), state0, starts)
+    assert torch.allclose(v, torch.stack(vals), rtol=1e-5, atol=1e-6)
+    assert torch.allclose(lp, torch.stack(lps), rtol=1e-5, atol=1e-5)
+    assert ent.shape == (T, n)
+
+
+def test_sequence_from_a_midway_state():
+    """Training starts a sequence from the state the collection stored at
+    its first step (RecurrentPPO.seq_states)."""
+    pol = _policy(1)
+    T, n = 10, 5
+    g = torch.Generator().manual_seed(2)
+    obs = torch.randn(T, n, 10, generator=g)
+    starts = torch.zeros(T, n)
+    state = pol.initial_state(n)
+    acts, lps, mid = [], [], None
+    for t in range(T):
+        if t == 4:
+            mid = state.clone()
+        a, _, lp, state = pol.act(obs[t], state, starts[t], generator=g)
+        acts.append(a)
+        lps.append(lp)
+    with torch.no_grad():
+        _, lp, _ = pol.evaluate(obs[4:], torch.stack(acts[4:]), mid, starts[4:])
+    assert torch.allclose(lp, torch.stack(lps[4:]), rtol=1e-5, atol=1e-5)
+
+
+def test_episode_start_zeroes_the_state():
+    pol = _policy(2)
+    n = 6
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(n, 10, generator=g)
+    busy = torch.randn(4, n, pol.hidden, generator=g)
+    with torch.no_grad():
+        v_start = pol.predict_values(x, busy, torch.ones(n))
+        v_fresh = pol.predict_values(x, pol.initial_state(n), torch.zeros(n))
+        v_busy = pol.predict_values(x, busy, torch.zeros(n))
+    assert torch.equal(v_start, v_fresh)
+    assert not torch.allclose(v_busy, v_fresh)
+
+
+def test_gradients_reach_both_lstms():
+    pol = _policy(3)
+    T, n = 6, 4
+    obs = torch.randn(T, n, 10)
+    v, lp, ent = pol.evaluate(obs, torch.randn(T, n, 3), pol.initial_state(n), torch.zeros(T, n))
+    (v.sum() + lp.sum()).backward()
+    assert pol.lstm_actor.weight_ih_l0.grad.abs().sum() > 0
+    assert pol.lstm_critic.weight_ih_l0.grad.abs().sum() > 0
+
+
+def test_configuration_checks():
+    class FakeSim:
+        obs_dim, n_envs, device = 10, 4, torch.device("cpu")
+    env = type("E", (), {"sim": FakeSim()})()
+    with pytest.raises(ValueError):
+        RecurrentPPO("MlpLstmPolicy", env, n_steps=20, seq_len=16)
+    with pytest.raises(ValueError):
+        RecurrentPPO("MlpLstmPolicy", env, n_steps=32, batch_size=64, seq_len=16,
+                     policy_kwargs={"shared_lstm": True})
+    with pytest.raises(ValueError):
+        RecurrentPPO("MlpPolicy", env, n_steps=32, batch_size=64, seq_len=16)

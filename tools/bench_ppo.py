@@ -69,6 +69,10 @@ def main():
     ap.add_argument("--lockstep-order", type=int, default=-1, help="salp_set_lockstep_order mode")
     ap.add_argument("--collect", default="auto", choices=("auto", "lockstep", "chained"),
                     help="collection: salp_step per env-step, or salp_collect (policy inside the kernel)")
+    ap.add_argument("--recurrent", action="store_true",
+                    help="RecurrentPPO with the MlpLstmPolicy (LSTM 256) of src/train_robot_recurrent_ppo.py")
+    ap.add_argument("--lstm-hidden", type=int, default=256)
+    ap.add_argument("--seq-len", type=int, default=16)
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -81,8 +85,13 @@ def main():
     from grasp_lab_salp_amd.vec_env import SalpVecEnv
     env = SalpVecEnv(a.n_envs, seed=0, env_id_offset=env_id_offset(rank, a.n_envs), infos=False)
     env.sim.set_lockstep_order(a.lockstep_order)
-    model = PPO("MlpPolicy", env, n_steps=a.n_steps, batch_size=a.batch_size, n_epochs=a.n_epochs, seed=0,
-                collect=a.collect)
+    if a.recurrent:
+        from grasp_lab_salp_amd.recurrent_ppo import RecurrentPPO
+        model = RecurrentPPO("MlpLstmPolicy", env, n_steps=a.n_steps, batch_size=a.batch_size, n_epochs=a.n_epochs,
+                             seed=0, seq_len=a.seq_len, policy_kwargs={"lstm_hidden_size": a.lstm_hidden})
+    else:
+        model = PPO("MlpPolicy", env, n_steps=a.n_steps, batch_size=a.batch_size, n_epochs=a.n_epochs, seed=0,
+                    collect=a.collect)
     model.learn(max(1, a.trend_iters) * a.n_steps * a.n_envs)   # warm-up (+ trend) iterations
     trend = list(model.history)
     for k in model.timing:
@@ -101,6 +110,8 @@ def main():
         res = {"metric": "PPO env-steps/sec (collect + GAE + update), config 5", "value": steps / el,
                "unit": "env-steps/s", "n_gpus": world, "n_envs_per_gpu": a.n_envs, "n_steps": a.n_steps,
                "batch_size": a.batch_size, "n_epochs": a.n_epochs, "iters": a.iters, "collect": model.collect,
+               "policy": (f"MlpLstmPolicy (LSTM {a.lstm_hidden}, seq_len {a.seq_len})" if a.recurrent
+                          else "MlpPolicy 64-64 tanh"),
                "timing_s": model.timing, "losses": model.logger,
                "history": model.history[h0:], "trend": trend if a.trend_iters else None,
                "diverged_envs_reset": model.nonfinite_resets,
