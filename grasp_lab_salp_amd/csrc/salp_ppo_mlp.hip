@@ -42,7 +42,6 @@ constexpr int NA = 3;                   // action dims
 constexpr int DP = 16;                  // observation columns in LDS (SALP_OBS_DIM_MAX <= 16)
 constexpr int TR = 64;                  // rows per tile
 constexpr int NT = 512;                 // threads per block of the row kernel (8 waves)
-constexpr int HS = H + 1;               // LDS row stride of the activations (bank spread)
 constexpr int NB_MAX = 256;             // row blocks (partials) at most
 constexpr int NADV = 256;               // blocks of k_mlp_adv_sums
 constexpr int NSTAT = 6;                // stats partials: pg, vf, clip, d log_std x 3
@@ -190,10 +189,10 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
     // gradient accumulators, kept over the block's tiles
     f32x16 gW2 = {};           // dW2[net][32 qa + crow(r, lh)][32 qb + lc]
     f32x4v gW1 = {};           // dW1[net][16 q + 4 (l >> 4) + r][l & 15]
-    float gB1 = 0.0f;          // db1[tid / H][tid % H]           (tid < 2 H)
-    float gB2 = 0.0f;          // db2[(tid - 2H) / H][tid % H]     (2 H <= tid < 4 H)
-    float gHead = 0.0f;        // dWa (tid < 192), dVw (192 <= tid < 256)
-    float gHeadB = 0.0f;       // dab (256 <= tid < 259), dvb (tid == 259)
+    float gB2 = 0.0f;          // db2[net][32 qa + lc], partial over this lane half's rows (qb == 0 waves)
+    float gB1 = 0.0f;          // db1[net][16 q + (l & 15)], partial over this lane group's rows
+    float gH[NA] = {0.0f, 0.0f, 0.0f};   // dWa[c][32 qb + lc] (actor) / dVw (critic, gH[0]): this lane's rows
+    double gHb[NA + 1] = {0.0, 0.0, 0.0, 0.0};   // dab[c], dvb: the rows of this heads thread
     double st[NSTAT] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     float ls[NA], var[NA];
     for (int j = 0; j < NA; ++j) {
@@ -201,17 +200,39 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
         const float sd = expf(ls[j]);
         var[j] = sd * sd;
     }
+    // this lane's columns of the heads (dz2 of its tile from registers)
+    const float aw0 = sAw[0][32 * qb + lc], aw1 = sAw[1][32 * qb + lc], aw2 = sAw[2][32 * qb + lc];
+    const float vw = sVw[32 * qb + lc];
     const float invB = 1.0f / (float)B, clip = (float)m.clip_range, vfc = (float)m.vf_coef;
     const float amean = sNorm[0], ainv = sNorm[1];
     const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_block;
     const int64_t r_end = r_begin + a.rows_per_block < B ? r_begin + a.rows_per_block : B;
+    static_assert(TR * DP == 2 * NT, "two observation entries per thread and tile");
+    // observations of a tile (gathered rows; padding rows are zero), loaded a
+    // tile ahead into registers: entries tid and tid + NT of the [TR][DP] tile
+    auto load_x = [&](int64_t row0, float* xv) {
+        const int64_t n = r_end - row0;
+        for (int u = 0; u < 2; ++u) {
+            const int e = tid + u * NT, r = e / DP, k = e % DP;
+            xv[u] = (r < n && k < D) ? m.obs[m.idx[row0 + r] * D + k] : 0.0f;
+        }
+    };
+    float xv[2];
+    if (r_begin < r_end) load_x(r_begin, xv);
 
     for (int64_t row0 = r_begin; row0 < r_end; row0 += TR) {
         const int nrows = (int)(r_end - row0 < TR ? r_end - row0 : TR);
-        // ---- observations of the tile (gathered rows; padding rows are zero)
-        for (int e = tid; e < TR * DP; e += NT) {
-            const int r = e / DP, k = e % DP;
-            sX[r][k] = (r < nrows && k < D) ? m.obs[m.idx[row0 + r] * D + k] : 0.0f;
+        for (int u = 0; u < 2; ++u) sX[(tid + u * NT) / DP][(tid + u * NT) % DP] = xv[u];
+        if (row0 + TR < r_end) load_x(row0 + TR, xv);
+        // the loss head's per-row inputs, issued now, used after both layers
+        const int hr = tid / 8, hp = tid % 8;
+        float r_act[NA] = {0.0f, 0.0f, 0.0f}, r_adv = 0.0f, r_olp = 0.0f, r_ret = 0.0f;
+        if (hp == 0 && hr < nrows) {
+            const int64_t b = m.idx[row0 + hr];
+            for (int j = 0; j < NA; ++j) r_act[j] = m.actions[3 * b + j];
+            r_adv = m.advantages[b];
+            r_olp = m.old_log_prob[b];
+            r_ret = m.returns[b];
         }
         __syncthreads();
         // ---- layer 1: h1 = tanh(x W1^T + b1)     (K = 16: 8 steps)
@@ -227,7 +248,8 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
             for (int r = 0; r < 16; ++r) sH1[net][32 * qa + crow(r, lh)][32 * qb + lc] = tanhf(acc[r]);
         }
         __syncthreads();
-        // ---- layer 2: h2 = tanh(h1 W2^T + b2)    (K = 64: 32 steps, k = 32 half + 4 s4 + e)
+        // ---- layer 2: h2 = tanh(h1 W2^T + b2)    (K = 64: 32 steps, k = 32 half + 4 s4 + e); h2 kept
+        float h2r[16];
         {
             const float b = sB2[net][32 * qb + lc];
             f32x16 acc = {b, b, b, b, b, b, b, b, b, b, b, b, b, b, b, b};
@@ -241,37 +263,38 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
                 acc = mfma32(x.w, y.w, acc);
             }
 #pragma unroll
-            for (int r = 0; r < 16; ++r) sH2[net][32 * qa + crow(r, lh)][32 * qb + lc] = tanhf(acc[r]);
+            for (int r = 0; r < 16; ++r) {
+                h2r[r] = tanhf(acc[r]);
+                sH2[net][32 * qa + crow(r, lh)][32 * qb + lc] = h2r[r];
+            }
         }
         __syncthreads();
         // ---- heads and the loss head: 8 threads per row
         {
-            const int r = tid / 8, p = tid % 8;
+            const int r = hr, p = hp;
             float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
             for (int qq = 0; qq < 8; ++qq) {
                 const int j = p * 8 + qq;
-                const float hp = sH2[0][r][j], hv = sH2[1][r][j];
-                s[0] = fmaf(hp, sAw[0][j], s[0]);
-                s[1] = fmaf(hp, sAw[1][j], s[1]);
-                s[2] = fmaf(hp, sAw[2][j], s[2]);
-                s[3] = fmaf(hv, sVw[j], s[3]);
+                const float h_p = sH2[0][r][j], h_v = sH2[1][r][j];
+                s[0] = fmaf(h_p, sAw[0][j], s[0]);
+                s[1] = fmaf(h_p, sAw[1][j], s[1]);
+                s[2] = fmaf(h_p, sAw[2][j], s[2]);
+                s[3] = fmaf(h_v, sVw[j], s[3]);
             }
             for (int o = 1; o < 8; o <<= 1)
                 for (int c = 0; c < 4; ++c) s[c] += __shfl_xor(s[c], o, 64);
             if (p == 0) {
                 float dmu[NA] = {0.0f, 0.0f, 0.0f}, dv = 0.0f;
                 if (r < nrows) {
-                    const int64_t b = m.idx[row0 + r];
                     float d[NA], lp = 0.0f;
                     for (int j = 0; j < NA; ++j) {
                         const float mu = s[j] + sAb[j];
-                        d[j] = m.actions[3 * b + j] - mu;
+                        d[j] = r_act[j] - mu;
                         lp += -(d[j] * d[j]) / (2.0f * var[j]) - ls[j] - kLogSqrt2Pi;
                     }
                     const float v = s[3] + sVb;
-                    const float adv = m.advantages[b];
-                    const float A = m.normalize_advantage ? (adv - amean) * ainv : adv;
-                    const float rt = expf(lp - m.old_log_prob[b]);
+                    const float A = m.normalize_advantage ? (r_adv - amean) * ainv : r_adv;
+                    const float rt = expf(lp - r_olp);
                     const float rc = fminf(fmaxf(rt, 1.0f - clip), 1.0f + clip);
                     const float p1 = A * rt, p2 = A * rc;
                     const float g1 = p1 < p2 ? 1.0f : (p1 == p2 ? 0.5f : 0.0f);
@@ -283,52 +306,52 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
                         dmu[j] = dlp * d[j] / var[j];
                         st[3 + j] += (double)(dlp * (d[j] * d[j] / var[j] - 1.0f));
                     }
-                    const float e = m.returns[b] - v;
+                    const float e = r_ret - v;
                     dv = vfc * (-2.0f * e * invB);
                     st[0] += (double)fminf(p1, p2);
                     st[1] += (double)(e * e);
                     st[2] += fabsf(rt - 1.0f) > clip ? 1.0 : 0.0;
                 }
-                for (int j = 0; j < NA; ++j) sDmu[r][j] = dmu[j];
+                for (int j = 0; j < NA; ++j) {
+                    sDmu[r][j] = dmu[j];
+                    gHb[j] += (double)dmu[j];
+                }
                 sDv[r] = dv;
+                gHb[NA] += (double)dv;
             }
         }
         __syncthreads();
-        // ---- head gradients (read h2 before dz2 overwrites it)
-        if (tid < NA * H) {
-            const int c = tid / H, j = tid % H;
-            float acc = 0.0f;
-            for (int r = 0; r < TR; ++r) acc = fmaf(sDmu[r][c], sH2[0][r][j], acc);
-            gHead += acc;
-        } else if (tid < NA * H + H) {
-            const int j = tid - NA * H;
-            float acc = 0.0f;
-            for (int r = 0; r < TR; ++r) acc = fmaf(sDv[r], sH2[1][r][j], acc);
-            gHead += acc;
-        } else if (tid < NA * H + H + NA + 1) {
-            const int c = tid - NA * H - H;
-            float acc = 0.0f;
-            for (int r = 0; r < TR; ++r) acc += c < NA ? sDmu[r][c] : sDv[r];
-            gHeadB += acc;
+        // ---- head weight gradients and dz2 = (head^T d) (1 - h2^2) of this wave's
+        //      tile, from the h2 it kept; dz2 replaces h2 (every reader of h2 is done)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = 32 * qa + crow(r, lh);
+            const float h = h2r[r];
+            float dh;
+            if (net == 0) {
+                const float d0 = sDmu[row][0], d1 = sDmu[row][1], d2 = sDmu[row][2];
+                gH[0] = fmaf(d0, h, gH[0]);
+                gH[1] = fmaf(d1, h, gH[1]);
+                gH[2] = fmaf(d2, h, gH[2]);
+                dh = fmaf(d2, aw2, fmaf(d1, aw1, d0 * aw0));
+            } else {
+                const float dv = sDv[row];
+                gH[0] = fmaf(dv, h, gH[0]);
+                dh = dv * vw;
+            }
+            sH2[net][row][32 * qb + lc] = dh * (1.0f - h * h);
         }
         __syncthreads();
-        // ---- dz2 = (head^T d) * (1 - h2^2), in place
-        for (int e = tid; e < 2 * TR * H; e += NT) {
-            const int n = e / (TR * H), r = (e / H) % TR, j = e % H;
-            const float h = sH2[n][r][j];
-            const float dh = n == 0 ? fmaf(sDmu[r][2], sAw[2][j], fmaf(sDmu[r][1], sAw[1][j], sDmu[r][0] * sAw[0][j]))
-                                    : sDv[r] * sVw[j];
-            sH2[n][r][j] = dh * (1.0f - h * h);
-        }
-        __syncthreads();
-        // ---- dW2 += dz2^T h1 (K = rows: r = 16 (s / 8) + 8 half + s % 8), db2 += sum dz2,
-        //      dh1 = dz2 W2 (K = units: 32 half + 4 s4 + e), dz1 = dh1 (1 - h1^2)
+        // ---- dW2 += dz2^T h1 (K = rows: r = 16 (s / 8) + 8 half + s % 8), db2 from the same
+        //      operand, dh1 = dz2 W2 (K = units: 32 half + 4 s4 + e), dz1 = dh1 (1 - h1^2)
         float dz1[16];
         {
 #pragma unroll
             for (int s = 0; s < 32; ++s) {
                 const int r = 16 * (s >> 3) + 8 * lh + (s & 7);
-                gW2 = mfma32(sH2[net][r][32 * qa + lc], sH1[net][r][32 * qb + lc], gW2);
+                const float z = sH2[net][r][32 * qa + lc];
+                gB2 += z;
+                gW2 = mfma32(z, sH1[net][r][32 * qb + lc], gW2);
             }
             f32x16 dh = {};
 #pragma unroll
@@ -345,29 +368,19 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
                 const float h = sH1[net][32 * qa + crow(r, lh)][32 * qb + lc];
                 dz1[r] = dh[r] * (1.0f - h * h);
             }
-            if (tid >= 2 * H && tid < 4 * H) {
-                const int n = (tid - 2 * H) / H, j = tid % H;
-                float acc = 0.0f;
-                for (int r = 0; r < TR; ++r) acc += sH2[n][r][j];
-                gB2 += acc;
-            }
         }
         __syncthreads();   // every read of h1 is done: dz1 replaces it
 #pragma unroll
         for (int r = 0; r < 16; ++r) sH1[net][32 * qa + crow(r, lh)][32 * qb + lc] = dz1[r];
         __syncthreads();
         // ---- dW1 += dz1^T x (16x16x4: wave q takes units 16 q .. 16 q + 15; r = 16 (l >> 4) + s),
-        //      db1 += sum dz1
+        //      db1 from the same operand
 #pragma unroll
         for (int s = 0; s < TR / 4; ++s) {
             const int r = 16 * (l >> 4) + s;
-            gW1 = mfma16(sH1[net][r][16 * q + (l & 15)], sX[r][l & 15], gW1);
-        }
-        if (tid < 2 * H) {
-            const int n = tid / H, u = tid % H;
-            float acc = 0.0f;
-            for (int r = 0; r < TR; ++r) acc += sH1[n][r][u];
-            gB1 += acc;
+            const float z = sH1[net][r][16 * q + (l & 15)];
+            gB1 += z;
+            gW1 = mfma16(z, sX[r][l & 15], gW1);
         }
         __syncthreads();
     }
@@ -382,13 +395,34 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
         if ((l & 15) < D)
 #pragma unroll
             for (int r = 0; r < 4; ++r) P[ow1 + (16 * q + 4 * (l >> 4) + r) * D + (l & 15)] = gW1[r];
+        // db2: the two lane halves' rows (waves qb == 0 saw every unit 32 qa + lc)
+        const float b2 = gB2 + __shfl_xor(gB2, 32, 64);
+        if (qb == 0 && lh == 0) P[a.L.off[net ? SALP_MLP_VF_B2 : SALP_MLP_PI_B2] + 32 * qa + lc] = b2;
+        // db1: the four lane groups' rows
+        float b1 = gB1 + __shfl_xor(gB1, 16, 64);
+        b1 += __shfl_xor(b1, 32, 64);
+        if (l < 16) P[a.L.off[net ? SALP_MLP_VF_B1 : SALP_MLP_PI_B1] + 16 * q + l] = b1;
     }
-    if (tid < 2 * H) P[a.L.off[tid / H ? SALP_MLP_VF_B1 : SALP_MLP_PI_B1] + tid % H] = gB1;
-    else if (tid < 4 * H) P[a.L.off[(tid - 2 * H) / H ? SALP_MLP_VF_B2 : SALP_MLP_PI_B2] + tid % H] = gB2;
-    if (tid < NA * H) P[a.L.off[SALP_MLP_ACT_W] + tid] = gHead;
-    else if (tid < NA * H + H) P[a.L.off[SALP_MLP_VAL_W] + tid - NA * H] = gHead;
-    else if (tid < NA * H + H + NA) P[a.L.off[SALP_MLP_ACT_B] + tid - NA * H - H] = gHeadB;
-    else if (tid == NA * H + H + NA) P[a.L.off[SALP_MLP_VAL_B]] = gHeadB;
+    // head weights: lane halves, then the two row-tile waves (qa) of each column block, via LDS
+    {
+        __shared__ float sHG[2][2][NA][H];   // [net][qa][c][unit]
+        float hg[NA];
+        for (int c = 0; c < NA; ++c) hg[c] = gH[c] + __shfl_xor(gH[c], 32, 64);
+        if (lh == 0)
+            for (int c = 0; c < (net == 0 ? NA : 1); ++c) sHG[net][qa][c][32 * qb + lc] = hg[c];
+        __syncthreads();
+        if (tid < NA * H) {
+            const int c = tid / H, j = tid % H;
+            P[a.L.off[SALP_MLP_ACT_W] + tid] = sHG[0][0][c][j] + sHG[0][1][c][j];
+        } else if (tid < NA * H + H) {
+            const int j = tid - NA * H;
+            P[a.L.off[SALP_MLP_VAL_W] + j] = sHG[1][0][0][j] + sHG[1][1][0][j];
+        }
+    }
+    for (int c = 0; c <= NA; ++c) {
+        const double t = block_sum_d(gHb[c], sRed, NT);
+        if (tid == 0) P[c < NA ? a.L.off[SALP_MLP_ACT_B] + c : a.L.off[SALP_MLP_VAL_B]] = (float)t;
+    }
     for (int k = 0; k < NSTAT; ++k) {
         const double t = block_sum_d(st[k], sRed, NT);
         if (tid == 0) a.stat_part[(int64_t)blockIdx.x * NSTAT + k] = t;

@@ -64,3 +64,51 @@ def test_step_and_reset_write_inside_their_buffers(n):
     bad = [i for i, b in enumerate(bufs) if not b.intact()]
     assert not bad and obs0.intact(), f"writes outside buffers {bad}"
     env.close()
+
+
+def test_rollout_step_random_and_collect_write_inside_their_buffers():
+    """The chained kernels (salp_rollout with every buffer, salp_step_random on
+    both of its paths, salp_collect with the guard on) over several launches
+    with auto-resets and diverged envs."""
+    from grasp_lab_salp_amd.ppo import ActorCritic, pack_policy
+    n, cap, K = 1000, 5, 12
+    env = BatchedSalpEnv(n, seed=9)
+    L = _lib.load()
+    od = env.obs_dim
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    bufs = []
+    B = _lib.SalpRolloutBuffers()
+    g = {"obs": Guarded((cap, n, od), torch.float32), "obs_before": Guarded((cap, n, od), torch.float32),
+         "actions": Guarded((cap, n, 3), torch.float32), "rewards": Guarded((cap, n), torch.float32),
+         "dones": Guarded((cap, n), torch.uint8), "steps_done": Guarded((n,), torch.int64)}
+    for k, v in g.items():
+        setattr(B, k, v.t.data_ptr())
+    B.capacity, B.max_steps, B.chunk = cap, 0, 97
+    for _ in range(3):
+        _lib.check(L.salp_rollout(env._h, 3000, ctypes.byref(B), st), env._h)
+    bufs += list(g.values())
+    for k in (1, 40):   # lock-step kernel, then the chained path with a step cap
+        rs = Guarded((n,), torch.float64)
+        _lib.check(L.salp_step_random(env._h, k, rs.ptr(), st), env._h)
+        bufs.append(rs)
+    pol = ActorCritic(od, 3).cuda()
+    w = Guarded((pack_policy(pol).numel(),), torch.float32)
+    pack_policy(pol, w.t)
+    R = _lib.SalpPolicyRollout(weights=w.t.data_ptr(), noise_seed=3, gamma=0.99, diverged_obs_abs=1e3,
+                               diverged_reward_abs=1e4, n_steps=K)
+    c = {"obs": Guarded((K, n, od), torch.float32), "actions": Guarded((K, n, 3), torch.float32),
+         "rewards": Guarded((K, n), torch.float32), "episode_starts": Guarded((K, n), torch.float32),
+         "values": Guarded((K, n), torch.float32), "log_probs": Guarded((K, n), torch.float32),
+         "episode_start": Guarded((n,), torch.float32, 1.0), "last_obs": Guarded((n, od), torch.float32),
+         "ep_stats": Guarded((4,), torch.float64), "diverged": Guarded((1,), torch.int64)}
+    _lib.check(L.salp_reset(env._h, None, c["last_obs"].ptr(), st), env._h)
+    for k, v in c.items():
+        setattr(R, k, v.t.data_ptr())
+    for _ in range(2):
+        _lib.check(L.salp_collect(env._h, ctypes.byref(R), st), env._h)
+    bufs += [w, *c.values()]
+    torch.cuda.synchronize()
+    bad = [i for i, b in enumerate(bufs) if not b.intact()]
+    assert not bad, f"writes outside buffers {bad}"
+    assert int(g["steps_done"].t.min()) > 0
+    env.close()
