@@ -9,7 +9,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRCS = [os.path.join(HERE, "csrc", f) for f in ("salp_kernels.hip", "salp_gae.hip", "salp_ppo.hip", "salp_ppo_mlp.hip",
-                                               "salp_sort.hip")]
+                                               "salp_sort.hip", "salp_lstm.hip")]
 OUT = os.path.join(HERE, "libsalp.so")
 ARCH = os.environ.get("SALP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -987,6 +987,13 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t salp_ppo_mlp_grads_l
 extern "C" __attribute__((visibility("hidden"))) hipError_t salp_ppo_mlp_apply_launch(const SalpPpoAdam* a,
                                                                                        void* stream);
 
+extern "C" __attribute__((visibility("hidden"))) hipError_t salp_lstm_fwd_launch(
+    int64_t m, int H, const float* G, const float* c_prev, const float* keep, float* h, float* c, float* act,
+    void* stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t salp_lstm_bwd_launch(
+    int64_t m, int H, const float* act, const float* c_prev, const float* keep, const float* c, const float* dh,
+    const float* dc, float* dG, float* dc_prev, void* stream);
+
 extern "C" __attribute__((visibility("hidden"))) hipError_t salp_sort_temp_bytes(int64_t n, size_t* bytes);
 extern "C" __attribute__((visibility("hidden"))) hipError_t salp_sort_launch(
     void* temp, size_t temp_bytes, const uint32_t* keys_in, uint32_t* keys_out, const int32_t* ids_in,
@@ -1382,6 +1389,26 @@ int salp_ppo_mlp_apply(const SalpPpoAdam* a, void* stream) {
     for (int t = 0; t < SALP_MLP_N_TENSORS; ++t)
         if (!a->params[t]) return fail(nullptr, SALP_EINVAL, "salp_ppo_mlp_apply: null parameter tensor");
     return check_hip(nullptr, salp_ppo_mlp_apply_launch(a, stream), "k_mlp_apply");
+}
+
+int salp_lstm_cell_forward(int64_t rows, int32_t hidden, const float* gates, const float* c_prev, const float* keep,
+                           float* h, float* c, float* act, void* stream) {
+    if (rows < 0 || hidden <= 0) return fail(nullptr, SALP_EINVAL, "salp_lstm_cell_forward: bad size");
+    if (!gates || !c_prev || !keep || !h || !c || !act)
+        return fail(nullptr, SALP_EINVAL, "salp_lstm_cell_forward: null buffer");
+    if (rows == 0) return SALP_OK;
+    return check_hip(nullptr, salp_lstm_fwd_launch(rows, hidden, gates, c_prev, keep, h, c, act, stream), "k_lstm_fwd");
+}
+
+int salp_lstm_cell_backward(int64_t rows, int32_t hidden, const float* act, const float* c_prev, const float* keep,
+                            const float* c, const float* dh, const float* dc, float* dgates, float* dc_prev,
+                            void* stream) {
+    if (rows < 0 || hidden <= 0) return fail(nullptr, SALP_EINVAL, "salp_lstm_cell_backward: bad size");
+    if (!act || !c_prev || !keep || !c || !dh || !dgates || !dc_prev)
+        return fail(nullptr, SALP_EINVAL, "salp_lstm_cell_backward: null buffer");
+    if (rows == 0) return SALP_OK;
+    return check_hip(nullptr, salp_lstm_bwd_launch(rows, hidden, act, c_prev, keep, c, dh, dc, dgates, dc_prev, stream),
+                     "k_lstm_bwd");
 }
 
 int salp_gae(int64_t n_steps, int64_t n_envs, const float* rewards, const float* values,

@@ -29,14 +29,64 @@ evaluated inside the simulation kernel; ``salp_collect`` runs the MLP
 policy), with the same divergence guard, episode statistics and HIP-event
 phase timings as :class:`~grasp_lab_salp_amd.ppo.PPO`.
 """
+import ctypes
 import math
 
 import torch
 from torch import nn
 
+from . import _lib
 from .ppo import PPO, _ortho, allreduce_gradients
 
-__all__ = ["RecurrentActorCritic", "RecurrentPPO"]
+__all__ = ["RecurrentActorCritic", "RecurrentPPO", "lstm_cell"]
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr() if t is not None else 0)
+
+
+class _LSTMCellFn(torch.autograd.Function):
+    """The elementwise part of an LSTM step through the HIP kernels of
+    salp_lstm_cell_forward / _backward (include/salp.h): one kernel each way
+    instead of ~8 / ~12 torch kernels."""
+
+    @staticmethod
+    def forward(ctx, gates, c_prev, keep):
+        m, h4 = gates.shape
+        H = h4 // 4
+        h = torch.empty((m, H), dtype=gates.dtype, device=gates.device)
+        c = torch.empty_like(h)
+        act = torch.empty_like(gates)
+        st = ctypes.c_void_p(torch.cuda.current_stream(gates.device).cuda_stream)
+        _lib.check(_lib.load().salp_lstm_cell_forward(m, H, _ptr(gates), _ptr(c_prev), _ptr(keep), _ptr(h), _ptr(c),
+                                                      _ptr(act), st))
+        ctx.save_for_backward(act, c_prev, keep, c)
+        return h, c
+
+    @staticmethod
+    def backward(ctx, dh, dc):
+        act, c_prev, keep, c = ctx.saved_tensors
+        m, H = c.shape
+        dh = torch.zeros_like(c) if dh is None else dh.contiguous()
+        dc = None if dc is None else dc.contiguous()
+        dg = torch.empty_like(act)
+        dcp = torch.empty_like(c_prev)
+        st = ctypes.c_void_p(torch.cuda.current_stream(c.device).cuda_stream)
+        _lib.check(_lib.load().salp_lstm_cell_backward(m, H, _ptr(act), _ptr(c_prev), _ptr(keep), _ptr(c), _ptr(dh),
+                                                       _ptr(dc), _ptr(dg), _ptr(dcp), st))
+        return dg, dcp, None
+
+
+def lstm_cell(gates, c_prev, keep):
+    """(h, c) of one LSTM step from the gate pre-activations [m, 4H] (i, f, g,
+    o), the previous cell state [m, H] and keep [m] (the state is zeroed where
+    keep is 0).  CUDA float32: the HIP kernels (fails if libsalp.so is
+    missing); CPU: the same equations in torch ops (the tests' path)."""
+    if gates.is_cuda:
+        return _LSTMCellFn.apply(gates.contiguous(), c_prev.contiguous(), keep.contiguous())
+    i, f, g, o = gates.chunk(4, 1)
+    c = torch.sigmoid(f) * (c_prev * keep.unsqueeze(1)) + torch.sigmoid(i) * torch.tanh(g)
+    return torch.sigmoid(o) * torch.tanh(c), c
 
 
 class RecurrentActorCritic(nn.Module):
@@ -71,9 +121,10 @@ class RecurrentActorCritic(nn.Module):
         """x [T, n, D] through `lstm` (torch's LSTM equations and parameter
         layout, gates i, f, g, o) from (h, c) [n, H]; the state is zeroed where
         starts[t] (an episode starts at step t), before step t.  The input
-        projection of all T steps is one GEMM; each step is one GEMM plus
-        elementwise work, all capturable in a HIP graph (a fused RNN library
-        call cannot reset states inside a sequence).
+        projection of all T steps is one GEMM; each step is one GEMM plus the
+        fused cell (lstm_cell: one HIP kernel each way), all capturable in a
+        HIP graph (a fused RNN library call cannot reset states inside a
+        sequence).
         Returns (outputs [T, n, H], h, c)."""
         T, n, D = x.shape
         gx = torch.addmm(lstm.bias_ih_l0 + lstm.bias_hh_l0, x.reshape(T * n, D),
@@ -81,11 +132,8 @@ class RecurrentActorCritic(nn.Module):
         w_hh = lstm.weight_hh_l0.t()
         outs = []
         for t in range(T):
-            keep = (1.0 - starts[t]).unsqueeze(1)
-            h, c = h * keep, c * keep
-            i, f, g, o = torch.addmm(gx[t], h, w_hh).chunk(4, 1)
-            c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(g)
-            h = torch.sigmoid(o) * torch.tanh(c)
+            keep = (1.0 - starts[t]).contiguous()
+            h, c = lstm_cell(torch.addmm(gx[t], h * keep.unsqueeze(1), w_hh), c, keep)
             outs.append(h)
         return torch.stack(outs), h, c
 

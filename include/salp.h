@@ -328,6 +328,21 @@ typedef struct SalpPpoAdam {
 } SalpPpoAdam;
 int salp_ppo_mlp_apply(const SalpPpoAdam* a, void* stream);
 
+/* The LSTM cell of RecurrentPPO's MlpLstmPolicy (sb3-contrib RecurrentPPO,
+ * src/train_robot_recurrent_ppo.py:85-107; grasp_lab_salp_amd/recurrent_ppo.py),
+ * elementwise part of one torch.nn.LSTM step with sb3-contrib's episode-start
+ * reset: gates [rows][4 hidden] = x W_ih^T + b + (h keep) W_hh^T (i, f, g, o),
+ * c_prev [rows][hidden], keep [rows] (1 - episode_start);
+ * c = sigmoid(f) c_prev keep + sigmoid(i) tanh(g), h = sigmoid(o) tanh(c);
+ * act [rows][4 hidden] receives the activated gates for the backward, which
+ * turns dh (and dc, or NULL) into dgates and dc_prev.  float32, caller's
+ * stream; not part of the reference's own API (its learner is sb3-contrib). */
+int salp_lstm_cell_forward(int64_t rows, int32_t hidden, const float* gates, const float* c_prev, const float* keep,
+                           float* h, float* c, float* act, void* stream);
+int salp_lstm_cell_backward(int64_t rows, int32_t hidden, const float* act, const float* c_prev, const float* keep,
+                            const float* c, const float* dh, const float* dc, float* dgates, float* dc_prev,
+                            void* stream);
+
 /* ------------------------------------------------ Robot / Nozzle level */
 /* The reference's Robot API for callers that drive the robot directly,
  * without the task env (src/compare_trajectories.py:120-168,

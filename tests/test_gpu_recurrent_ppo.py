@@ -60,3 +60,34 @@ def test_recurrent_graphed_update_equals_eager():
         env.close()
     assert torch.isfinite(out[0]).all()
     assert torch.equal(out[0], out[1])
+
+
+def test_lstm_cell_kernels_equal_torch_lstm():
+    """salp_lstm_cell_forward / _backward against torch.nn.LSTM's step (gates
+    from the same GEMMs) with resets: h, c and every gradient within float32
+    rounding (the kernels use expf / tanhf where torch uses its own)."""
+    from grasp_lab_salp_amd.recurrent_ppo import lstm_cell
+    torch.manual_seed(0)
+    m, D, H = 300, 10, 64
+    lstm = torch.nn.LSTM(D, H).cuda()
+    x = torch.randn(m, D, device="cuda")
+    h0 = torch.randn(m, H, device="cuda")
+    c0 = torch.randn(m, H, device="cuda", requires_grad=True)
+    keep = (torch.rand(m, device="cuda") > 0.3).float()
+    g = torch.addmm(lstm.bias_ih_l0 + lstm.bias_hh_l0, x, lstm.weight_ih_l0.t()) + (h0 * keep[:, None]) @ lstm.weight_hh_l0.t()
+    g1 = g.detach().clone().requires_grad_(True)
+    h, c = lstm_cell(g1, c0, keep)
+    with torch.no_grad():
+        o, (hr, cr) = lstm(x[None], ((h0 * keep[:, None])[None], (c0 * keep[:, None])[None]))
+    assert torch.allclose(h, hr[0], rtol=1e-5, atol=1e-6) and torch.allclose(c, cr[0], rtol=1e-5, atol=1e-6)
+    dh, dc = torch.randn_like(h), torch.randn_like(c)
+    (h * dh + c * dc).sum().backward()
+    g2 = g.detach().clone().requires_grad_(True)
+    c02 = c0.detach().clone().requires_grad_(True)
+    i, f, gg, o2 = g2.chunk(4, 1)
+    c2 = torch.sigmoid(f) * (c02 * keep[:, None]) + torch.sigmoid(i) * torch.tanh(gg)
+    h2 = torch.sigmoid(o2) * torch.tanh(c2)
+    (h2 * dh + c2 * dc).sum().backward()
+    assert torch.allclose(g1.grad, g2.grad, rtol=1e-4, atol=1e-6)
+    assert torch.allclose(c0.grad, c02.grad, rtol=1e-4, atol=1e-6)
+    assert bool((c0.grad[keep == 0] == 0).all())

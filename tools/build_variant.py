@@ -34,7 +34,8 @@ def main():
         s = open(hit[0]).read().replace(old, new)
         open(hit[0], "w").write(s)
     out = os.path.join(ROOT, "exp_build", f"libsalp_{name}.so")
-    srcs = [os.path.join(d, "grasp_lab_salp_amd", "csrc", f) for f in ("salp_kernels.hip", "salp_gae.hip", "salp_ppo.hip", "salp_ppo_mlp.hip", "salp_sort.hip")]
+    srcs = [os.path.join(d, "grasp_lab_salp_amd", "csrc", f) for f in ("salp_kernels.hip", "salp_gae.hip", "salp_ppo.hip", "salp_ppo_mlp.hip", "salp_sort.hip",
+                                                                     "salp_lstm.hip")]
     extra = os.environ.get("EXTRA_FLAGS", "").split()   # e.g. "-mllvm -amdgpu-sched-strategy=max-ilp"
     subprocess.run([B.HIPCC, *B.FLAGS, *extra, "-o", out, *srcs], check=True)
     print(out)

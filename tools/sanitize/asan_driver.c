@@ -177,6 +177,9 @@ static void abi_host_paths(void) {
     CHECK(salp_ppo_mlp_offset(10, SALP_MLP_N_TENSORS) == salp_ppo_mlp_num_params(10));
     CHECK(salp_ppo_mlp_num_params(0) == -1 && salp_ppo_mlp_workspace_doubles(0, 10) == -1);
     CHECK(salp_ppo_mlp_grads(NULL, NULL) == SALP_EINVAL);
+    CHECK(salp_lstm_cell_forward(4, 0, NULL, NULL, NULL, NULL, NULL, NULL, NULL) == SALP_EINVAL);
+    CHECK(salp_lstm_cell_forward(4, 8, NULL, NULL, NULL, NULL, NULL, NULL, NULL) == SALP_EINVAL);
+    CHECK(salp_lstm_cell_backward(-1, 8, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL) == SALP_EINVAL);
     {
         SalpPpoMinibatch mb;
         memset(&mb, 0, sizeof mb);
