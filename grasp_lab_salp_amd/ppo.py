@@ -393,6 +393,7 @@ class PPO:
                                     capturable=self.use_graphs, fused=fused or None)
         self._graph = None
         self._graph_warm = 0
+        self._epoch_graph = None   # fused step, one GPU: one graph per epoch of minibatches
         self._g_clip = None
         self._collect_stream = None
         self.n_steps, self.batch_size, self.n_epochs = int(n_steps), int(batch_size), int(n_epochs)
@@ -721,6 +722,8 @@ class PPO:
         still captured afresh per update when the buffer leaves an eager tail
         minibatch (its GEMMs run on the replay stream)."""
         N = self.n_steps * self.n_envs
+        if self.fused_update and self.use_graphs and not self._multi and N % self.batch_size == 0:
+            return self._train_epoch_graphs()
         if not self.fused_update and N % self.batch_size:
             self._graph, self._graph_warm = None, 0   # eager tail minibatch: recapture (see docstring)
         acc = torch.zeros(4, device=self.device)
@@ -740,6 +743,36 @@ class PPO:
             acc = acc + self._g_acc
             self._g_acc.zero_()
         vals = (acc / max(steps, 1)).tolist()
+        return dict(zip(("pg_loss", "vf_loss", "entropy", "clip_frac"), vals))
+
+    def _train_epoch_graphs(self):
+        """train() for the fused step on one GPU: every minibatch of an epoch
+        reads its rows from a slice of one persistent permutation, so the whole
+        epoch (4 kernels per minibatch) is one HIP graph, captured once and
+        replayed n_epochs times per update after a fresh permutation is drawn
+        into it.  The same kernels in the same order as minibatch by minibatch
+        (no per-minibatch index copy, no per-minibatch launch from Python)."""
+        N = self.n_steps * self.n_envs
+        bs = self.batch_size
+        fresh = False
+        if self._epoch_graph is None or self._g_clip != self._clip():
+            if self._epoch_graph is None:
+                self._perm = torch.empty(N, dtype=torch.int64, device=self.device)
+                self._g_acc = torch.zeros(4, device=self.device)
+            torch.randperm(N, generator=self.gen, device=self.device, out=self._perm)
+            self._g_clip = self._clip()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for s in range(0, N, bs):
+                    self._fused_minibatch(self._perm[s:s + bs], self._g_acc)
+            self._epoch_graph = g
+            fresh = True
+        for e in range(self.n_epochs):
+            if not (fresh and e == 0):   # the capture's permutation serves the first epoch
+                torch.randperm(N, generator=self.gen, device=self.device, out=self._perm)
+            self._epoch_graph.replay()
+        vals = (self._g_acc / (self.n_epochs * (N // bs))).tolist()
+        self._g_acc.zero_()
         return dict(zip(("pg_loss", "vf_loss", "entropy", "clip_frac"), vals))
 
     def learn(self, total_timesteps, log_interval=1):

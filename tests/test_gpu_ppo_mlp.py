@@ -141,42 +141,28 @@ def test_fused_step_equals_torch_clip_and_adam():
 
 
 def test_fused_graph_is_kept_and_equals_eager():
-    """PPO with the fused step replays one graph captured in the first update
-    for every later update; in the third update a replay equals the same
-    minibatch run eagerly from the same state, bit for bit (no atomics), and
-    everything stays finite."""
-    env = SalpVecEnv(32768, seed=0, infos=False)
-    model = PPO("MlpPolicy", env, n_steps=8, batch_size=32768, n_epochs=2, seed=0, use_graphs=True)
-    assert model.fused_update
-    seen, graphs = [], []
-    inner = model._graphed_minibatch
-
-    def state():
-        return [t.detach().clone() for t in model._mlp_tensors] + [model._f_m.clone(), model._f_v.clone(),
-                                                          model._f_step.clone()]
-
-    def put(vals):
-        with torch.no_grad():
-            for d, v in zip(model._mlp_tensors + [model._f_m, model._f_v, model._f_step], vals):
-                d.copy_(v)
-
-    def check(idx):
-        graphs.append(id(model._graph))
-        if model._graph is None or len(model.history) < 2 or seen:
-            return inner(idx)
-        pre = state()
-        inner(idx)
-        post = state()
-        put(pre)
-        model._fused_minibatch(model._g_idx, torch.zeros(4, device="cuda"))
-        eager = state()
-        seen.append(all(torch.equal(x, y) for x, y in zip(post, eager)))
-        put(post)
-
-    model._graphed_minibatch = check
-    model.learn(3 * 8 * 32768)
-    assert seen and seen[0]
-    assert len(set(graphs[1:])) == 1, "one graph, kept across updates"
-    assert all(bool(torch.isfinite(p).all()) for p in model.policy.parameters())
-    for row in model.history:
-        assert np.isfinite(row["vf_loss"]) and np.isfinite(row["pg_loss"])
+    """PPO with the fused step on one GPU replays one graph per epoch, captured
+    in the first update and kept for every later one; three iterations leave
+    exactly (bit for bit: no atomics) the parameters, Adam state and losses of
+    the same learner stepping every minibatch eagerly, and stay finite."""
+    out = []
+    for graphs in (True, False):
+        env = SalpVecEnv(32768, seed=0, infos=False)
+        model = PPO("MlpPolicy", env, n_steps=8, batch_size=32768, n_epochs=2, seed=0, use_graphs=graphs)
+        assert model.fused_update and model.use_graphs == graphs
+        ids = []
+        for _ in range(3):
+            model.learn(model.num_timesteps + 8 * 32768)
+            ids.append(id(model._epoch_graph))
+        if graphs:
+            assert model._epoch_graph is not None and len(set(ids)) == 1, "one epoch graph, kept across updates"
+        out.append(([t.detach().clone() for t in model._mlp_tensors] + [model._f_m.clone(), model._f_v.clone(),
+                                                                        model._f_step.clone()],
+                    [(r["pg_loss"], r["vf_loss"]) for r in model.history]))
+        env.close()
+    (sg, hg), (se, he) = out
+    assert all(torch.equal(x, y) for x, y in zip(sg, se))
+    assert hg == he
+    assert all(bool(torch.isfinite(t).all()) for t in sg)
+    for pg, vf in hg:
+        assert np.isfinite(vf) and np.isfinite(pg)
