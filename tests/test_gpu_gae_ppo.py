@@ -96,7 +96,8 @@ def test_graphed_update_equals_eager_update():
         model = PPO("MlpPolicy", env, n_steps=8, batch_size=256, n_epochs=3, seed=1, use_graphs=graphs)
         model.learn(total_timesteps=8 * 256)   # one rollout + one update (identical data)
         params.append(torch.cat([p.detach().reshape(-1) for p in model.policy.parameters()]).cpu())
-        assert model.use_graphs == graphs and (model._graph is not None) == graphs
+        captured = model._graph is not None or model._epoch_graph is not None
+        assert model.use_graphs == graphs and captured == graphs
         env.close()
     # same data and steps; only Adam's capturable (tensor-step) arithmetic differs by rounding
     assert torch.allclose(params[0], params[1], rtol=1e-4, atol=1e-6)
