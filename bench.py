@@ -240,7 +240,8 @@ def ppo_leg(a, rank, world, dev):
             "unit": "env-steps/s", "n_envs_per_gpu": n, "n_steps": T, "batch_size": 32768, "n_epochs": 10,
             "collect": "chained (salp_collect)" if T >= 256 else "lockstep (salp_step)",
             "iteration_s": el_max, "timing_s_max_over_ranks": timing,
-            "gae_kernel": gae, "policy": "SB3 MlpPolicy 64-64 tanh (the reference's RecurrentPPO uses LSTM-256)"}
+            "gae_kernel": gae, "policy": "SB3 MlpPolicy 64-64 tanh (the reference's LSTM-256 RecurrentPPO: "
+                                         "grasp_lab_salp_amd.recurrent_ppo, tools/bench_ppo.py --recurrent)"}
 
 
 def dry_run(a, world, rank):

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define SALP_ABI_VERSION 6
+#define SALP_ABI_VERSION 7
 
 #define SALP_MAX_OBSTACLES 4
 #define SALP_OBS_DIM_MAX (6 + 2 * SALP_MAX_OBSTACLES)

@@ -51,13 +51,21 @@ def _equal_up_to_nan_payload(a, b):
     return bool(np.all(same | both))
 
 
-@pytest.mark.parametrize("n,n_steps,gamma", [(300, 7, 0.99), (1024, 5, 0.9)])
-def test_collect_replays_on_the_lockstep_path(n, n_steps, gamma):
+ALL_RAND = dict(dynamics=True, disturbances=True, actions=True, observations=True, latency=True)
+
+
+@pytest.mark.parametrize("n,n_steps,gamma,rand", [(300, 7, 0.99, False), (1024, 5, 0.9, False), (500, 6, 0.99, True)])
+def test_collect_replays_on_the_lockstep_path(n, n_steps, gamma, rand):
+    """rand: every randomisation switch on (k_rollout<RAND, POL>; the twin's
+    salp_step draws from the same Philox streams)."""
     p = default_params()
     p.max_cycles = 3        # timeouts inside the collection: the bootstrap path runs
     env = BatchedSalpEnv(n, params=p, seed=23)
-    obs0 = env.reset()
     twin = BatchedSalpEnv(n, params=p, seed=23)
+    if rand:
+        env.set_randomization(**ALL_RAND)
+        twin.set_randomization(**ALL_RAND)
+    obs0 = env.reset()
     twin.set_state(env.get_state())
     pol = _policy(1)
     w = pack_policy(pol)
