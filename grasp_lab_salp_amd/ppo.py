@@ -293,6 +293,10 @@ def timeout_bootstrap(reward, terminated, truncated, terminal_value, gamma):
 # A legitimate step stays far inside these bounds: |reward| <= ~1.5e3 (success
 # +500, progress and penalties of a body moving < 1 m/s within 5 m of the
 # target), |obs| < 1e2 (metres, m/s, rad).
+# HIP-graph capture checks only this thread's calls: with RCCL, the process
+# group's watchdog thread keeps querying events while a rank captures
+_CAPTURE_MODE = "thread_local"
+
 DIVERGED_OBS_ABS = 1e3
 DIVERGED_REWARD_ABS = 1e4
 
@@ -677,13 +681,13 @@ class PPO:
             self._g_clip = self._clip()
             self._graph = torch.cuda.CUDAGraph()
             if self._multi:   # gradient graph | all-reduce (eager) | clip + Adam graph
-                with torch.cuda.graph(self._graph):
+                with torch.cuda.graph(self._graph, capture_error_mode=_CAPTURE_MODE):
                     self._fused_minibatch(self._g_idx, self._g_acc, part="grads")
                 self._graph_apply = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self._graph_apply):
+                with torch.cuda.graph(self._graph_apply, capture_error_mode=_CAPTURE_MODE):
                     self._fused_minibatch(self._g_idx, self._g_acc, part="apply")
             else:
-                with torch.cuda.graph(self._graph):
+                with torch.cuda.graph(self._graph, capture_error_mode=_CAPTURE_MODE):
                     self._minibatch(self._g_idx, self._g_acc)
             self._graph_warm = 1
         elif self._graph is None:
@@ -702,7 +706,7 @@ class PPO:
                 return
             self.opt.zero_grad(set_to_none=True)
             self._graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._graph):
+            with torch.cuda.graph(self._graph, capture_error_mode=_CAPTURE_MODE):
                 self._minibatch(self._g_idx, self._g_acc)
         else:
             self._g_idx.copy_(idx)
@@ -762,7 +766,7 @@ class PPO:
             torch.randperm(N, generator=self.gen, device=self.device, out=self._perm)
             self._g_clip = self._clip()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
                 for s in range(0, N, bs):
                     self._fused_minibatch(self._perm[s:s + bs], self._g_acc)
             self._epoch_graph = g
