@@ -92,7 +92,12 @@ def main():
     else:
         model = PPO("MlpPolicy", env, n_steps=a.n_steps, batch_size=a.batch_size, n_epochs=a.n_epochs, seed=0,
                     collect=a.collect)
-    model.learn(max(1, a.trend_iters) * a.n_steps * a.n_envs)   # warm-up (+ trend) iterations
+    # warm-up (+ trend) iterations, one learn() call each so that a long trend
+    # reports progress on stderr (a GPU job silent for minutes looks hung)
+    for it in range(max(1, a.trend_iters)):
+        model.learn((it + 1) * a.n_steps * a.n_envs)
+        if rank == 0:
+            print(json.dumps(model.history[-1]), file=sys.stderr, flush=True)
     trend = list(model.history)
     for k in model.timing:
         model.timing[k] = 0.0
