@@ -388,7 +388,7 @@ class PPO:
         # HIP graphs: on one rank always; with several ranks for the fused step
         # only, as two graphs (gradient, then clip + Adam) with the RCCL
         # all-reduce of the flat gradient between them, outside any capture
-        graphs_ok = not multi or self.fused_update
+        graphs_ok = self.device.type == "cuda" and (not multi or self.fused_update)
         self.use_graphs = graphs_ok if use_graphs is None else bool(use_graphs) and graphs_ok
         # fused Adam on the GPU: one kernel for all parameters instead of ~4
         # elementwise kernels per parameter tensor (capturable either way)
