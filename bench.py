@@ -283,8 +283,16 @@ def main(argv=None):
             dist.destroy_process_group()
         return
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # SALP_BENCH_REHEARSAL=1: the multi-rank code path on fewer GPUs than
+        # ranks (ranks share devices, gloo carries the reductions and the PPO
+        # gradient all-reduce): for checking the N-rank run on a one-GPU box;
+        # its timings mean nothing
+        rehearsal = os.environ.get("SALP_BENCH_REHEARSAL") == "1"
+        torch.cuda.set_device(local % torch.cuda.device_count() if rehearsal else local)
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         if dist.get_world_size() != world:
             raise SystemExit("process group size differs from WORLD_SIZE")
     else:
