@@ -92,6 +92,27 @@ __device__ __forceinline__ double block_sum_d(double v, double* sh, int nthreads
     return t;   // valid in thread 0
 }
 
+// K block sums at once, in a fixed order (the wave's xor tree, then the
+// waves in order), broadcast to every thread through sh [nthreads / 64][K].
+template <int K>
+__device__ __forceinline__ void block_sums(double (&v)[K], double* sh, int nthreads) {
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k] += __shfl_xor(v[k], o, 64);
+    const int w = threadIdx.x / 64, l = threadIdx.x % 64;
+    __syncthreads();
+    if (l == 0)
+#pragma unroll
+        for (int k = 0; k < K; ++k) sh[w * K + k] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        double t = 0.0;
+        for (int ww = 0; ww < nthreads / 64; ++ww) t += sh[ww * K + k];
+        v[k] = t;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_mlp_adv_sums(int64_t B, const int64_t* __restrict__ idx,
                                                       const float* __restrict__ adv, double* __restrict__ part) {
     __shared__ double sh[4];
@@ -146,16 +167,34 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
     __shared__ __attribute__((aligned(16))) float sH2[2][TR][HS2];  // h2, then dz2 in place
     __shared__ float sDmu[TR][NA], sDv[TR];
     __shared__ float sNorm[2];
-    __shared__ double sRed[NT / 64];
+    __shared__ double sRed[NT / 64 * (NA + 1 + NSTAT)];
 
-    for (int e = tid; e < 2 * H * DP; e += NT) {
-        const int net = e / (H * DP), u = (e / DP) % H, k = e % DP;
-        const float* w = m.params[net ? SALP_MLP_VF_W1 : SALP_MLP_PI_W1];
-        sW1[net][u][k] = k < D ? w[u * D + k] : 0.0f;
-    }
-    for (int e = tid; e < 2 * H * H; e += NT) {
-        const int net = e / (H * H), j = (e / H) % H, k = e % H;
-        sW2[net][j][k] = m.params[net ? SALP_MLP_VF_W2 : SALP_MLP_PI_W2][j * H + k];
+    // weights into LDS: every load of a thread is issued before its stores
+    // (one L2 round trip instead of one per element)
+    {
+        constexpr int N1 = 2 * H * DP / NT, N2 = 2 * H * H / NT;
+        static_assert(N1 * NT == 2 * H * DP && N2 * NT == 2 * H * H, "whole staging rounds");
+        float v1[N1], v2[N2];
+#pragma unroll
+        for (int q = 0; q < N1; ++q) {
+            const int e = tid + q * NT, net = e / (H * DP), u = (e / DP) % H, k = e % DP;
+            v1[q] = k < D ? m.params[net ? SALP_MLP_VF_W1 : SALP_MLP_PI_W1][u * D + k] : 0.0f;
+        }
+#pragma unroll
+        for (int q = 0; q < N2; ++q) {
+            const int e = tid + q * NT, net = e / (H * H);
+            v2[q] = m.params[net ? SALP_MLP_VF_W2 : SALP_MLP_PI_W2][e % (H * H)];
+        }
+#pragma unroll
+        for (int q = 0; q < N1; ++q) {
+            const int e = tid + q * NT;
+            sW1[e / (H * DP)][(e / DP) % H][e % DP] = v1[q];
+        }
+#pragma unroll
+        for (int q = 0; q < N2; ++q) {
+            const int e = tid + q * NT;
+            sW2[e / (H * H)][(e / H) % H][e % H] = v2[q];
+        }
     }
     for (int e = tid; e < 2 * H; e += NT) {
         const int net = e / H, j = e % H;
@@ -168,19 +207,21 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
         sAb[tid] = m.params[SALP_MLP_ACT_B][tid];
         sLs[tid] = m.params[SALP_MLP_LOG_STD][tid];
     }
-    if (tid == 0) {
-        sVb = m.params[SALP_MLP_VAL_B][0];
-        float mean = 0.0f, inv = 1.0f;
-        if (m.normalize_advantage && B > 1) {
-            double s = 0.0, q = 0.0;
-            for (int k = 0; k < NADV; ++k) { s += a.adv_part[2 * k]; q += a.adv_part[2 * k + 1]; }
-            const double mu = s / (double)B;
-            const double var = fmax(q - s * mu, 0.0) / (double)(B - 1);
-            mean = (float)mu;
-            inv = 1.0f / ((float)sqrt(var) + 1e-8f);
+    if (tid == 0) sVb = m.params[SALP_MLP_VAL_B][0];
+    // advantage mean / std of the minibatch from k_mlp_adv_sums' partials, summed by the block
+    if (m.normalize_advantage && B > 1) {
+        static_assert(NADV <= NT, "one advantage partial per thread");
+        double sq[2] = {tid < NADV ? a.adv_part[2 * tid] : 0.0, tid < NADV ? a.adv_part[2 * tid + 1] : 0.0};
+        block_sums(sq, sRed, NT);
+        if (tid == 0) {
+            const double mu = sq[0] / (double)B;
+            const double var = fmax(sq[1] - sq[0] * mu, 0.0) / (double)(B - 1);
+            sNorm[0] = (float)mu;
+            sNorm[1] = 1.0f / ((float)sqrt(var) + 1e-8f);
         }
-        sNorm[0] = mean;
-        sNorm[1] = inv;
+    } else if (tid == 0) {
+        sNorm[0] = 0.0f;
+        sNorm[1] = 1.0f;
     }
     __syncthreads();
 
@@ -419,13 +460,16 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
             P[a.L.off[SALP_MLP_VAL_W] + j] = sHG[1][0][0][j] + sHG[1][1][0][j];
         }
     }
-    for (int c = 0; c <= NA; ++c) {
-        const double t = block_sum_d(gHb[c], sRed, NT);
-        if (tid == 0) P[c < NA ? a.L.off[SALP_MLP_ACT_B] + c : a.L.off[SALP_MLP_VAL_B]] = (float)t;
-    }
-    for (int k = 0; k < NSTAT; ++k) {
-        const double t = block_sum_d(st[k], sRed, NT);
-        if (tid == 0) a.stat_part[(int64_t)blockIdx.x * NSTAT + k] = t;
+    // head biases and the loss statistics: one block reduction for all ten
+    double red[NA + 1 + NSTAT];
+#pragma unroll
+    for (int c = 0; c <= NA; ++c) red[c] = gHb[c];
+#pragma unroll
+    for (int k = 0; k < NSTAT; ++k) red[NA + 1 + k] = st[k];
+    block_sums(red, sRed, NT);
+    if (tid == 0) {
+        for (int c = 0; c <= NA; ++c) P[c < NA ? a.L.off[SALP_MLP_ACT_B] + c : a.L.off[SALP_MLP_VAL_B]] = (float)red[c];
+        for (int k = 0; k < NSTAT; ++k) a.stat_part[(int64_t)blockIdx.x * NSTAT + k] = red[NA + 1 + k];
     }
 }
 
