@@ -532,12 +532,13 @@ __device__ __forceinline__ RolloutArgs fresh_args() {
 #define SALP_ROLLOUT_RESEAT 1
 #endif
 
-// Position of the k-th set bit of the 256-bit mask m[0..3] (k < popcount).
+// Position of the k-th set bit of the kBlock-bit mask m[0..kBlock/64-1] (k < popcount).
 __device__ __forceinline__ int nth_set_lane(const uint64_t* m, int k) {
+    constexpr int NW = kBlock / 64;
     int base = 0;
-    uint64_t w = m[3];
+    uint64_t w = m[NW - 1];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
+    for (int j = 0; j < NW - 1; ++j) {
         const int c = __popcll(m[j]);
         if (k < c) {
             w = m[j];

@@ -536,7 +536,7 @@ static_assert((int64_t)NT_APPLY * AP_MAX >= 2 * (H * DP + H + H * H + H) + NA * 
               "the flat gradient of obs_dim <= 16 fits one apply block");
 __global__ __launch_bounds__(NT_APPLY) void k_mlp_apply(SalpPpoAdam o, Layout L) {
     __shared__ double sh[NT_APPLY / 64];
-    __shared__ float s_coef, s_step;
+    __shared__ float s_coef;
     __shared__ float* s_base[SALP_MLP_N_TENSORS];   // params[t] - off[t]: p indexes it directly
     __shared__ int s_off[SALP_MLP_N_TENSORS];
 #pragma unroll
@@ -546,6 +546,7 @@ __global__ __launch_bounds__(NT_APPLY) void k_mlp_apply(SalpPpoAdam o, Layout L)
             s_off[t] = (int)L.off[t];
         }
     const int P = (int)L.off[SALP_MLP_N_TENSORS];
+    const float step = o.step[0] + 1.0f;   // issued with the parameter loads, not after the norm
     __syncthreads();
     float g[AP_MAX], m1[AP_MAX], v1[AP_MAX], w1[AP_MAX];
     float* wp[AP_MAX];
@@ -575,11 +576,10 @@ __global__ __launch_bounds__(NT_APPLY) void k_mlp_apply(SalpPpoAdam o, Layout L)
             coef = coef < 1.0f ? coef : 1.0f;
         }
         s_coef = coef;
-        s_step = o.step[0] + 1.0f;
         if (o.grad_norm) o.grad_norm[0] = total;
     }
     __syncthreads();
-    const float coef = s_coef, step = s_step;
+    const float coef = s_coef;
     const float b1 = (float)o.beta1, b2 = (float)o.beta2, lr = (float)o.lr, eps = (float)o.eps;
     const float bc1 = 1.0f - powf(b1, step), bc2 = 1.0f - powf(b2, step);
     const float step_size = lr / bc1, bc2_sqrt = sqrtf(bc2);

@@ -1,7 +1,7 @@
-"""Where k_mlp_fwd_bwd spends its time, per wave and phase (staging, tile
-loads, layer 1, layer 2, loss head, dz2 + head gradients, dW2 + dh1, dz1
-store, dW1, partial writes).  Needs an instrumented build exporting
-salp_debug_mlp_prof (s_memtime deltas per wave; SALP_LIB=...)."""
+"""Where k_mlp_fwd_bwd spends its time, per wave and phase (phase i ends at
+the kernel's i-th __syncthreads(), the last one at the kernel's end).  Needs
+the instrumented build of tools/build_mlp_prof.py (SALP_LIB=
+exp_build/libsalp_mlpprof.so)."""
 import ctypes
 import json
 import os
@@ -15,8 +15,7 @@ from grasp_lab_salp_amd import _lib  # noqa: E402
 from grasp_lab_salp_amd.ppo import PPO  # noqa: E402
 from grasp_lab_salp_amd.vec_env import SalpVecEnv  # noqa: E402
 
-PHASES = ["staging", "tile_loads", "layer1", "layer2", "loss_head", "dz2_headgrads", "dW2_dh1", "dz1_store", "dW1",
-          "partials"]
+NPH = 24   # tools/build_mlp_prof.py: phase i ends at the kernel's i-th __syncthreads()
 
 
 def main():
@@ -31,11 +30,11 @@ def main():
     L = _lib.load()
     L.salp_debug_mlp_prof.argtypes = [ctypes.c_void_p, ctypes.c_int64]
     n = 256 * 8
-    a = np.zeros((n, 10), dtype=np.uint64)
+    a = np.zeros((n, NPH), dtype=np.uint64)
     assert L.salp_debug_mlp_prof(a.ctypes.data, n) == 0
     w = a.astype(np.float64)
     tot = w.sum(1)
-    print(json.dumps({"phases": PHASES, "frac": [round(float(x), 4) for x in w.sum(0) / tot.sum()],
+    print(json.dumps({"frac_by_barrier": [round(float(x), 4) for x in w.sum(0) / tot.sum()],
                       "wave_cycles_mean": float(tot.mean())}))
 
 
