@@ -125,6 +125,8 @@ SIGNATURES = {
     "salp_collect": (ctypes.c_int, [_H, ctypes.POINTER(SalpPolicyRollout), _V]),
     "salp_lstm_cell_forward": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, _V, _V, _V, _V, _V, _V, _V]),
     "salp_lstm_cell_backward": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
+    "salp_lstm_step_forward": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
+    "salp_lstm_step_backward": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32] + [_V] * 11),
     "salp_set_lockstep_order": (ctypes.c_int, [_H, ctypes.c_int]),
     "salp_robot_reset": (ctypes.c_int, [_H, _V, _V]),
     "salp_nozzle_set_angles": (ctypes.c_int, [_H, _V, _V]),

@@ -989,11 +989,11 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t salp_ppo_mlp_apply_l
                                                                                        void* stream);
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t salp_lstm_fwd_launch(
-    int64_t m, int H, const float* G, const float* c_prev, const float* keep, float* h, float* c, float* act,
-    void* stream);
+    int64_t m, int H, const float* G, const float* GX, const float* c_prev, const float* keep, const float* keep_next,
+    float* h, float* c, float* act, float* hk, void* stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t salp_lstm_bwd_launch(
     int64_t m, int H, const float* act, const float* c_prev, const float* keep, const float* c, const float* dh,
-    const float* dc, float* dG, float* dc_prev, void* stream);
+    const float* dhk_next, const float* keep_next, const float* dc, float* dG, float* dc_prev, void* stream);
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t salp_sort_temp_bytes(int64_t n, size_t* bytes);
 extern "C" __attribute__((visibility("hidden"))) hipError_t salp_sort_launch(
@@ -1398,7 +1398,21 @@ int salp_lstm_cell_forward(int64_t rows, int32_t hidden, const float* gates, con
     if (!gates || !c_prev || !keep || !h || !c || !act)
         return fail(nullptr, SALP_EINVAL, "salp_lstm_cell_forward: null buffer");
     if (rows == 0) return SALP_OK;
-    return check_hip(nullptr, salp_lstm_fwd_launch(rows, hidden, gates, c_prev, keep, h, c, act, stream), "k_lstm_fwd");
+    return check_hip(nullptr, salp_lstm_fwd_launch(rows, hidden, gates, nullptr, c_prev, keep, nullptr, h, c, act,
+                                                   nullptr, stream), "k_lstm_fwd");
+}
+
+int salp_lstm_step_forward(int64_t rows, int32_t hidden, const float* gates, const float* gx, const float* c_prev,
+                           const float* keep, const float* keep_next, float* h, float* c, float* act, float* hk_next,
+                           void* stream) {
+    if (rows < 0 || hidden <= 0) return fail(nullptr, SALP_EINVAL, "salp_lstm_step_forward: bad size");
+    if (!gates || !c_prev || !keep || !h || !c || !act)
+        return fail(nullptr, SALP_EINVAL, "salp_lstm_step_forward: null buffer");
+    if (!keep_next != !hk_next)
+        return fail(nullptr, SALP_EINVAL, "salp_lstm_step_forward: keep_next and hk_next go together");
+    if (rows == 0) return SALP_OK;
+    return check_hip(nullptr, salp_lstm_fwd_launch(rows, hidden, gates, gx, c_prev, keep, keep_next, h, c, act,
+                                                   hk_next, stream), "k_lstm_fwd");
 }
 
 int salp_lstm_cell_backward(int64_t rows, int32_t hidden, const float* act, const float* c_prev, const float* keep,
@@ -1408,8 +1422,21 @@ int salp_lstm_cell_backward(int64_t rows, int32_t hidden, const float* act, cons
     if (!act || !c_prev || !keep || !c || !dh || !dgates || !dc_prev)
         return fail(nullptr, SALP_EINVAL, "salp_lstm_cell_backward: null buffer");
     if (rows == 0) return SALP_OK;
-    return check_hip(nullptr, salp_lstm_bwd_launch(rows, hidden, act, c_prev, keep, c, dh, dc, dgates, dc_prev, stream),
-                     "k_lstm_bwd");
+    return check_hip(nullptr, salp_lstm_bwd_launch(rows, hidden, act, c_prev, keep, c, dh, nullptr, nullptr, dc, dgates,
+                                                   dc_prev, stream), "k_lstm_bwd");
+}
+
+int salp_lstm_step_backward(int64_t rows, int32_t hidden, const float* act, const float* c_prev, const float* keep,
+                            const float* c, const float* d_out, const float* dhk_next, const float* keep_next,
+                            const float* dc, float* dgates, float* dc_prev, void* stream) {
+    if (rows < 0 || hidden <= 0) return fail(nullptr, SALP_EINVAL, "salp_lstm_step_backward: bad size");
+    if (!act || !c_prev || !keep || !c || !d_out || !dgates || !dc_prev)
+        return fail(nullptr, SALP_EINVAL, "salp_lstm_step_backward: null buffer");
+    if (!dhk_next != !keep_next)
+        return fail(nullptr, SALP_EINVAL, "salp_lstm_step_backward: dhk_next and keep_next go together");
+    if (rows == 0) return SALP_OK;
+    return check_hip(nullptr, salp_lstm_bwd_launch(rows, hidden, act, c_prev, keep, c, d_out, dhk_next, keep_next, dc,
+                                                   dgates, dc_prev, stream), "k_lstm_bwd");
 }
 
 int salp_gae(int64_t n_steps, int64_t n_envs, const float* rewards, const float* values,

@@ -21,20 +21,35 @@ namespace {
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // act [m][4H]: the activated gates (i, f, g, o) for the backward pass
+// Sequence steps (salp_lstm_step_forward): GX (the input projection, or null)
+// is added to G here instead of by a copy before the GEMM, and hk = h keep_next
+// (the next step's GEMM operand, when keep_next is not null) is written too.
 __global__ __launch_bounds__(256) void k_lstm_fwd(int64_t m, int H, const float* __restrict__ G,
+                                                  const float* __restrict__ GX,
                                                   const float* __restrict__ c_prev, const float* __restrict__ keep,
+                                                  const float* __restrict__ keep_next,
                                                   float* __restrict__ h, float* __restrict__ c,
-                                                  float* __restrict__ act) {
+                                                  float* __restrict__ act, float* __restrict__ hk) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= m * H) return;
     const int64_t r = e / H;
     const int u = (int)(e - r * H);
     const float* g = G + r * 4 * H;
-    const float ig = sigm(g[u]), fg = sigm(g[H + u]), gg = tanhf(g[2 * H + u]), og = sigm(g[3 * H + u]);
+    float gi = g[u], gf = g[H + u], gc = g[2 * H + u], go = g[3 * H + u];
+    if (GX) {
+        const float* x = GX + r * 4 * H;
+        gi = x[u] + gi;
+        gf = x[H + u] + gf;
+        gc = x[2 * H + u] + gc;
+        go = x[3 * H + u] + go;
+    }
+    const float ig = sigm(gi), fg = sigm(gf), gg = tanhf(gc), og = sigm(go);
     const float ck = c_prev[e] * keep[r];
     const float cn = fg * ck + ig * gg;
     c[e] = cn;
-    h[e] = og * tanhf(cn);
+    const float hn = og * tanhf(cn);
+    h[e] = hn;
+    if (keep_next) hk[e] = hn * keep_next[r];
     float* a = act + r * 4 * H;
     a[u] = ig;
     a[H + u] = fg;
@@ -44,9 +59,13 @@ __global__ __launch_bounds__(256) void k_lstm_fwd(int64_t m, int H, const float*
 
 // dh, dc: gradients of the step's h and c outputs (dc may be null: zero);
 // dG [m][4H] the gate pre-activations' gradient, dc_prev [m][H] c_prev's
+// Sequence steps (salp_lstm_step_backward): dh = d_out + dhk_next keep_next
+// (the gradient through the next step's GEMM operand, when dhk_next is not null).
 __global__ __launch_bounds__(256) void k_lstm_bwd(int64_t m, int H, const float* __restrict__ act,
                                                   const float* __restrict__ c_prev, const float* __restrict__ keep,
                                                   const float* __restrict__ c, const float* __restrict__ dh,
+                                                  const float* __restrict__ dhk_next,
+                                                  const float* __restrict__ keep_next,
                                                   const float* __restrict__ dc, float* __restrict__ dG,
                                                   float* __restrict__ dc_prev) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -58,7 +77,7 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(int64_t m, int H, const float*
     const float kp = keep[r];
     const float ck = c_prev[e] * kp;
     const float tc = tanhf(c[e]);
-    const float dhe = dh[e];
+    const float dhe = dhk_next ? dh[e] + dhk_next[e] * keep_next[r] : dh[e];
     const float dcn = (dc ? dc[e] : 0.0f) + dhe * og * (1.0f - tc * tc);
     float* d = dG + r * 4 * H;
     d[u] = dcn * gg * ig * (1.0f - ig);
@@ -71,19 +90,18 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(int64_t m, int H, const float*
 }  // namespace
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t salp_lstm_fwd_launch(
-    int64_t m, int H, const float* G, const float* c_prev, const float* keep, float* h, float* c, float* act,
-    void* stream) {
+    int64_t m, int H, const float* G, const float* GX, const float* c_prev, const float* keep, const float* keep_next,
+    float* h, float* c, float* act, float* hk, void* stream) {
     const int64_t n = m * H;
-    hipLaunchKernelGGL(k_lstm_fwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, m, H, G,
-                       c_prev, keep, h, c, act);
+    hipLaunchKernelGGL(k_lstm_fwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, m, H, G, GX,
+                       c_prev, keep, keep_next, h, c, act, hk);
     return hipGetLastError();
 }
-
 extern "C" __attribute__((visibility("hidden"))) hipError_t salp_lstm_bwd_launch(
     int64_t m, int H, const float* act, const float* c_prev, const float* keep, const float* c, const float* dh,
-    const float* dc, float* dG, float* dc_prev, void* stream) {
+    const float* dhk_next, const float* keep_next, const float* dc, float* dG, float* dc_prev, void* stream) {
     const int64_t n = m * H;
     hipLaunchKernelGGL(k_lstm_bwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, m, H,
-                       act, c_prev, keep, c, dh, dc, dG, dc_prev);
+                       act, c_prev, keep, c, dh, dhk_next, keep_next, dc, dG, dc_prev);
     return hipGetLastError();
 }

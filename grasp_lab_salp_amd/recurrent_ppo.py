@@ -36,7 +36,7 @@ import torch
 from torch import nn
 
 from . import _lib
-from .ppo import PPO, _ortho, allreduce_gradients
+from .ppo import PPO, SplitKLinear, _ortho, allreduce_gradients
 
 __all__ = ["RecurrentActorCritic", "RecurrentPPO", "lstm_cell"]
 
@@ -77,6 +77,88 @@ class _LSTMCellFn(torch.autograd.Function):
         return dg, dcp, None
 
 
+class _SharedInputProjFn(torch.autograd.Function):
+    """y[t, k] = x[t] @ w[k]: the input projection of every step t of the
+    networks k, which share the input x [T, 1, n, K] (observations: no
+    gradient); w [1, nets, K, N].  The weight gradient sum_t x_t^T dy[t, k] has
+    K = 11 rows and T n = 32 768 reduction steps per minibatch: as one GEMM per
+    network the library runs it on a handful of workgroups (~140 us); here the
+    steps are the batch of one batched GEMM and the T products are summed
+    (same math, another summation order)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x)
+        return torch.matmul(x, w)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x,) = ctx.saved_tensors
+        return None, torch.matmul(x.transpose(-1, -2), gy).sum(0, keepdim=True)
+
+
+class _LSTMPairSeqFn(torch.autograd.Function):
+    """Both LSTMs (actor, critic) over a whole sequence, with the backward pass
+    through time written out instead of recorded step by step (CUDA float32).
+
+    Inputs: gx [T, 2, n, 4H] (input projection + bias), w_hh [2, H, 4H],
+    h0 / c0 [2, n, H], keep [T, n] and keep2 [T, 2n] (1 - episode start).
+    Outputs: h of every step [T, 2, n, H] and the last c [2, n, H].
+    Per step forward: G = hk W_hh (one batched GEMM for both networks), then
+    the cell kernel (salp_lstm_step_forward), which adds gx and writes the
+    next step's hk = h keep; backward: the cell kernel (salp_lstm_step_backward,
+    dh = d_out + d hk_next keep_next), then d hk = dG W_hh^T (one batched
+    GEMM).  The recurrent weight gradient
+    sum_t hk_t^T dG_t is one batched GEMM over all steps at the end, and dG
+    of every step is written straight into the input projection's gradient,
+    where step-by-step autograd ran 16 weight-gradient GEMMs and the
+    accumulations between them."""
+
+    @staticmethod
+    def forward(ctx, gx, w_hh, h0, c0, keep, keep2):
+        T, _, n, H4 = gx.shape
+        H = H4 // 4
+        out = gx.new_empty(T, 2, n, H)
+        hk = gx.new_empty(T, 2, n, H)
+        act = gx.new_empty(T, 2, n, H4)
+        cs = gx.new_empty(T + 1, 2, n, H)
+        cs[0].copy_(c0)
+        g = gx.new_empty(2, n, H4)
+        lib = _lib.load()
+        st = ctypes.c_void_p(torch.cuda.current_stream(gx.device).cuda_stream)
+        torch.mul(h0, keep[0].view(1, n, 1), out=hk[0])
+        for t in range(T):
+            torch.bmm(hk[t], w_hh, out=g)
+            nxt = t + 1 < T
+            _lib.check(lib.salp_lstm_step_forward(2 * n, H, _ptr(g), _ptr(gx[t]), _ptr(cs[t]), _ptr(keep2[t]),
+                                                  _ptr(keep2[t + 1] if nxt else None), _ptr(out[t]),
+                                                  _ptr(cs[t + 1]), _ptr(act[t]), _ptr(hk[t + 1] if nxt else None), st))
+        ctx.save_for_backward(w_hh, hk, act, cs, keep, keep2)
+        return out, cs[T]
+
+    @staticmethod
+    def backward(ctx, d_out, d_cT):
+        w_hh, hk, act, cs, keep, keep2 = ctx.saved_tensors
+        T, _, n, H = hk.shape
+        lib = _lib.load()
+        st = ctypes.c_void_p(torch.cuda.current_stream(hk.device).cuda_stream)
+        dG = torch.empty_like(act)
+        d_out = torch.zeros_like(hk) if d_out is None else d_out.contiguous()
+        dc = None if d_cT is None else d_cT.contiguous()
+        dhk = None                         # d hk[t + 1]
+        w_t = w_hh.transpose(1, 2).contiguous()
+        for t in range(T - 1, -1, -1):
+            dcp = torch.empty_like(d_out[t])
+            _lib.check(lib.salp_lstm_step_backward(2 * n, H, _ptr(act[t]), _ptr(cs[t]), _ptr(keep2[t]),
+                                                   _ptr(cs[t + 1]), _ptr(d_out[t]), _ptr(dhk),
+                                                   _ptr(keep2[t + 1] if dhk is not None else None), _ptr(dc),
+                                                   _ptr(dG[t]), _ptr(dcp), st))
+            dhk = torch.bmm(dG[t], w_t)
+            dc = dcp
+        d_w = torch.matmul(hk.transpose(-1, -2), dG).sum(0)
+        return dG, d_w, dhk * keep[0].view(1, n, 1), dc, None, None
+
+
 def lstm_cell(gates, c_prev, keep):
     """(h, c) of one LSTM step from the gate pre-activations [m, 4H] (i, f, g,
     o), the previous cell state [m, H] and keep [m] (the state is zeroed where
@@ -103,14 +185,14 @@ class RecurrentActorCritic(nn.Module):
         def mlp():
             layers, d = [], self.hidden
             for h in net_arch:
-                layers += [_ortho(nn.Linear(d, h), math.sqrt(2)), nn.Tanh()]
+                layers += [_ortho(SplitKLinear(d, h), math.sqrt(2)), nn.Tanh()]
                 d = h
             return nn.Sequential(*layers), d
 
         self.pi_net, d_pi = mlp()
         self.vf_net, d_vf = mlp()
-        self.action_net = _ortho(nn.Linear(d_pi, act_dim), 0.01)
-        self.value_net = _ortho(nn.Linear(d_vf, 1), 1.0)
+        self.action_net = _ortho(SplitKLinear(d_pi, act_dim), 0.01)
+        self.value_net = _ortho(SplitKLinear(d_vf, 1), 1.0)
         self.log_std = nn.Parameter(torch.zeros(act_dim))
 
     def initial_state(self, n, device=None):
@@ -127,31 +209,74 @@ class RecurrentActorCritic(nn.Module):
         sequence).
         Returns (outputs [T, n, H], h, c)."""
         T, n, D = x.shape
+        # unbind, not gx[t]: the backward of T separate selects would zero-fill
+        # and add T full-size [T, n, 4H] gradients; unbind's is one stack
         gx = torch.addmm(lstm.bias_ih_l0 + lstm.bias_hh_l0, x.reshape(T * n, D),
-                         lstm.weight_ih_l0.t()).view(T, n, -1)
+                         lstm.weight_ih_l0.t()).view(T, n, -1).unbind(0)
         w_hh = lstm.weight_hh_l0.t()
+        keeps = (1.0 - starts).unbind(0)
         outs = []
         for t in range(T):
-            keep = (1.0 - starts[t]).contiguous()
+            keep = keeps[t]
             h, c = lstm_cell(torch.addmm(gx[t], h * keep.unsqueeze(1), w_hh), c, keep)
             outs.append(h)
         return torch.stack(outs), h, c
 
+    def _run_pair(self, x, state, starts):
+        """_run of the actor and the critic LSTM together (same input, same
+        episode starts): every GEMM batched over the two networks (bmm), one
+        cell launch per step for both.  state [4, n, H].
+        Returns (actor outputs, critic outputs [T, n, H], new state)."""
+        T, n, D = x.shape
+        la, lc = self.lstm_actor, self.lstm_critic
+        w_hh = torch.stack([la.weight_hh_l0, lc.weight_hh_l0]).transpose(1, 2)        # [2, H, 4H]
+        # input projection of all T steps, the bias folded in as a ones column
+        wb = torch.stack([torch.cat([la.weight_ih_l0.t(), (la.bias_ih_l0 + la.bias_hh_l0).unsqueeze(0)]),
+                          torch.cat([lc.weight_ih_l0.t(), (lc.bias_ih_l0 + lc.bias_hh_l0).unsqueeze(0)])])
+        xa = torch.cat([x, x.new_ones(T, n, 1)], 2).unsqueeze(1)                       # [T, 1, n, D + 1]
+        if torch.is_grad_enabled():
+            gx = _SharedInputProjFn.apply(xa, wb.unsqueeze(0))
+        else:
+            gx = torch.matmul(xa, wb.unsqueeze(0))                                     # [T, 2, n, 4H]
+        keep1 = (1.0 - starts)                                                        # [T, n]
+        keep2 = keep1.repeat(1, 2)                                                    # [T, 2n]: both nets
+        if x.is_cuda:
+            out, c = _LSTMPairSeqFn.apply(gx, w_hh, state[0::2].contiguous(), state[1::2].contiguous(), keep1,
+                                          keep2)
+            h = out[T - 1]
+            oa, oc = out.unbind(1)
+            return oa, oc, torch.stack([h[0], c[0], h[1], c[1]])
+        gx = gx.unbind(0)
+        keeps = keep1.unbind(0)
+        keeps2 = keep2.unbind(0)
+        h, c = state[0::2], state[1::2].reshape(2 * n, -1)                            # [2, n, H], [2n, H]
+        outs = []
+        for t in range(T):
+            g = torch.baddbmm(gx[t], h * keeps[t].view(1, n, 1), w_hh)
+            hf, c = lstm_cell(g.view(2 * n, -1), c, keeps2[t])
+            h = hf.view(2, n, -1)
+            outs.append(h)
+        out = torch.stack(outs, 1)                                                    # [2, T, n, H]
+        c = c.view(2, n, -1)
+        return out[0], out[1], torch.stack([h[0], c[0], h[1], c[1]])
+
     def forward_seq(self, obs, state, starts, critic=True):
         """Latents of a sequence: obs [T, n, D], state [4, n, H], starts [T, n].
         Returns (actor latent [T, n, H], critic latent or None, new state)."""
+        if critic:
+            return self._run_pair(obs, state, starts)
         lp, hp, cp = self._run(self.lstm_actor, obs, state[0], state[1], starts)
-        if not critic:
-            return lp, None, torch.stack([hp, cp, state[2], state[3]])
-        lv, hv, cv = self._run(self.lstm_critic, obs, state[2], state[3], starts)
-        return lp, lv, torch.stack([hp, cp, hv, cv])
+        return lp, None, torch.stack([hp, cp, state[2], state[3]])
 
     def _dist(self, latent_pi):
-        mean = self.action_net(self.pi_net(latent_pi))
+        # the heads on [rows, H] (SplitKLinear's split-K weight gradient)
+        mean = self.action_net(self.pi_net(latent_pi.reshape(-1, latent_pi.shape[-1])))
+        mean = mean.view(*latent_pi.shape[:-1], -1)
         return torch.distributions.Normal(mean, self.log_std.exp().expand_as(mean), validate_args=False)
 
     def _value(self, latent_vf):
-        return self.value_net(self.vf_net(latent_vf)).squeeze(-1)
+        v = self.value_net(self.vf_net(latent_vf.reshape(-1, latent_vf.shape[-1])))
+        return v.view(latent_vf.shape[:-1])
 
     @torch.no_grad()
     def act(self, obs, state, episode_starts, generator=None):

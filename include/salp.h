@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define SALP_ABI_VERSION 7
+#define SALP_ABI_VERSION 8
 
 #define SALP_MAX_OBSTACLES 4
 #define SALP_OBS_DIM_MAX (6 + 2 * SALP_MAX_OBSTACLES)
@@ -342,6 +342,18 @@ int salp_lstm_cell_forward(int64_t rows, int32_t hidden, const float* gates, con
 int salp_lstm_cell_backward(int64_t rows, int32_t hidden, const float* act, const float* c_prev, const float* keep,
                             const float* c, const float* dh, const float* dc, float* dgates, float* dc_prev,
                             void* stream);
+/* One step of a whole-sequence pass (the training pass of both LSTMs,
+ * recurrent_ppo._LSTMPairSeqFn).  Forward: the cell of gates + gx (gx, the
+ * input projection with the bias, may be NULL), and hk_next = h keep_next (the
+ * next step's recurrent GEMM operand; keep_next and hk_next both NULL or
+ * both set).  Backward: the cell's backward for dh = d_out + dhk_next keep_next
+ * (dhk_next = d hk_next; dhk_next and keep_next both NULL or both set). */
+int salp_lstm_step_forward(int64_t rows, int32_t hidden, const float* gates, const float* gx, const float* c_prev,
+                           const float* keep, const float* keep_next, float* h, float* c, float* act, float* hk_next,
+                           void* stream);
+int salp_lstm_step_backward(int64_t rows, int32_t hidden, const float* act, const float* c_prev, const float* keep,
+                            const float* c, const float* d_out, const float* dhk_next, const float* keep_next,
+                            const float* dc, float* dgates, float* dc_prev, void* stream);
 
 /* ------------------------------------------------ Robot / Nozzle level */
 /* The reference's Robot API for callers that drive the robot directly,

@@ -91,3 +91,36 @@ def test_lstm_cell_kernels_equal_torch_lstm():
     assert torch.allclose(g1.grad, g2.grad, rtol=1e-4, atol=1e-6)
     assert torch.allclose(c0.grad, c02.grad, rtol=1e-4, atol=1e-6)
     assert bool((c0.grad[keep == 0] == 0).all())
+
+
+def test_pair_sequence_bptt_equals_stepwise_autograd():
+    """The training pass of both LSTMs as one hand-written BPTT
+    (_LSTMPairSeqFn: batched GEMMs for the two networks, one recurrent weight
+    gradient over all steps) against each LSTM run step by step under autograd
+    (RecurrentActorCritic._run): outputs, the new state and every parameter
+    gradient within float32 rounding, with episode starts inside the sequence
+    and a state that starts mid-episode."""
+    from grasp_lab_salp_amd.recurrent_ppo import RecurrentActorCritic
+    torch.manual_seed(0)
+    T, n, D, H = 16, 512, 10, 64
+    pol = RecurrentActorCritic(D, 3, lstm_hidden_size=H).cuda()
+    x = torch.randn(T, n, D, device="cuda")
+    state = torch.randn(4, n, H, device="cuda")
+    starts = (torch.rand(T, n, device="cuda") < 0.1).float()
+    w_out = torch.randn(T, n, H, device="cuda")
+    params = list(pol.lstm_actor.parameters()) + list(pol.lstm_critic.parameters())
+
+    def grads(lp, lv, new):
+        loss = (lp * w_out).sum() + (lv * w_out.flip(0)).sum() + (new[1] * new[3]).sum()
+        g = torch.autograd.grad(loss, params)
+        return torch.cat([t.reshape(-1) for t in g])
+
+    lp, lv, new = pol.forward_seq(x, state, starts)
+    g_pair = grads(lp, lv, new)
+    a, ha, ca = pol._run(pol.lstm_actor, x, state[0], state[1], starts)
+    v, hv, cv = pol._run(pol.lstm_critic, x, state[2], state[3], starts)
+    g_step = grads(a, v, torch.stack([ha, ca, hv, cv]))
+    assert torch.allclose(lp, a, rtol=1e-4, atol=1e-5) and torch.allclose(lv, v, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(new, torch.stack([ha, ca, hv, cv]), rtol=1e-4, atol=1e-5)
+    scale = float(g_step.abs().max())
+    assert float((g_pair - g_step).abs().max()) <= 1e-4 * scale, (float((g_pair - g_step).abs().max()), scale)

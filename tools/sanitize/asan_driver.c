@@ -180,6 +180,9 @@ static void abi_host_paths(void) {
     CHECK(salp_lstm_cell_forward(4, 0, NULL, NULL, NULL, NULL, NULL, NULL, NULL) == SALP_EINVAL);
     CHECK(salp_lstm_cell_forward(4, 8, NULL, NULL, NULL, NULL, NULL, NULL, NULL) == SALP_EINVAL);
     CHECK(salp_lstm_cell_backward(-1, 8, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL) == SALP_EINVAL);
+    CHECK(salp_lstm_step_forward(4, 8, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL) == SALP_EINVAL);
+    CHECK(salp_lstm_step_backward(4, -1, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL) ==
+          SALP_EINVAL);
     {
         SalpPpoMinibatch mb;
         memset(&mb, 0, sizeof mb);
