@@ -92,7 +92,7 @@ SD Params pin_params(const Params& P) {
                  "+v"(v.com_mass_sum), "+v"(v.P1000tv), "+v"(v.end_aspect), "+v"(v.aspect_den));
     asm volatile("" : "+v"(v.sk.S1), "+v"(v.sk.S2), "+v"(v.sk.S3), "+v"(v.sk.S4), "+v"(v.sk.S5),
                  "+v"(v.sk.S6), "+v"(v.sk.C1), "+v"(v.sk.C2), "+v"(v.sk.C3), "+v"(v.sk.C4), "+v"(v.sk.C5),
-                 "+v"(v.sk.C6));
+                 "+v"(v.sk.C6), "+v"(v.sk.R_INV), "+v"(v.sk.R_P1), "+v"(v.sk.R_P1T));
     return v;
 }
 

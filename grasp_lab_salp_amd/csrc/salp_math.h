@@ -160,12 +160,14 @@ SM_QUAL void sm_np_sincosf(float x, float* s_out, float* c_out) {
  * pinning each use separately costs a v_mov_b64 per coefficient per call. */
 typedef struct {
     double S1, S2, S3, S4, S5, S6, C1, C2, C3, C4, C5, C6;
+    double R_INV, R_P1, R_P1T;   /* sm_rem_pio2's common-path constants: 2/pi, pio2_1, pio2_1t */
 } SmPoly;
 SM_QUAL SmPoly sm_poly(void) {
     SmPoly k = {-1.66666666666666324348e-01, 8.33333333332248946124e-03, -1.98412698298579493134e-04,
                 2.75573137070700676789e-06,  -2.50507602534068634195e-08, 1.58969099521155010221e-10,
                 4.16666666666666019037e-02,  -1.38888888888741095749e-03, 2.48015872894767294178e-05,
-                -2.75573143513906633035e-07, 2.08757232129817482790e-09,  -1.13596475577881948265e-11};
+                -2.75573143513906633035e-07, 2.08757232129817482790e-09,  -1.13596475577881948265e-11,
+                6.36619772367581382433e-01,  1.57079632673412561417e+00,  6.07710050650619224932e-11};
     return k;
 }
 /* fdlibm's kernels with the polynomial steps written as sm_mad: with
@@ -197,9 +199,8 @@ SM_QUAL double sm_ksin(double x, double y, int iy) { return sm_ksin_p(x, y, iy, 
 SM_QUAL double sm_kcos(double x, double y) { return sm_kcos_p(x, y, sm_poly()); }
 /* Cody-Waite reduction for |x| < 2^20*pi/2 (fdlibm __ieee754_rem_pio2,
  * medium case).  Returns n with x = n*pi/2 + (y0 + y1). */
-SM_QUAL int sm_rem_pio2(double x, double* y0, double* y1) {
-    const double invpio2 = 6.36619772367581382433e-01,
-                 pio2_1 = 1.57079632673412561417e+00, pio2_1t = 6.07710050650619224932e-11,
+SM_QUAL int sm_rem_pio2_p(double x, double* y0, double* y1, SmPoly K) {
+    const double invpio2 = K.R_INV, pio2_1 = K.R_P1, pio2_1t = K.R_P1T,
                  pio2_2 = 6.07710050630396597660e-11, pio2_2t = 2.02226624879595063154e-21,
                  pio2_3 = 2.02226624871116645580e-21, pio2_3t = 8.47842766036889956997e-32;
     double fn = rint(x * invpio2);
@@ -234,6 +235,7 @@ SM_QUAL int sm_rem_pio2(double x, double* y0, double* y1) {
     const double q = fn - 4.0 * floor(fn * 0.25);
     return q == q ? (int)q : 0;
 }
+SM_QUAL int sm_rem_pio2(double x, double* y0, double* y1) { return sm_rem_pio2_p(x, y0, y1, sm_poly()); }
 SM_QUAL void sm_sincos_p(double x, double* s_out, double* c_out, SmPoly K) {
     int32_t ix = sm_hi(x) & 0x7fffffff;
     /* |x| <= pi/4, or x is NaN: the kernels return NaN for it as the
@@ -246,7 +248,7 @@ SM_QUAL void sm_sincos_p(double x, double* s_out, double* c_out, SmPoly K) {
         return;
     }
     double y0, y1;
-    int n = sm_rem_pio2(x, &y0, &y1);
+    int n = sm_rem_pio2_p(x, &y0, &y1, K);
     double s = sm_ksin_p(y0, y1, 1, K), c = sm_kcos_p(y0, y1, K);
     switch (n & 3) {
         case 0: *s_out = s; *c_out = c; break;
@@ -264,7 +266,7 @@ SM_QUAL void sm_sincos_p(double x, double* s_out, double* c_out, SmPoly K) {
 SM_QUAL void sm_sincos_nb_p(double x, double* s_out, double* c_out, SmPoly K) {
     const int small = (sm_hi(x) & 0x7fffffff) <= 0x3fe921fb;
     double y0, y1;
-    int n = sm_rem_pio2(x, &y0, &y1);
+    int n = sm_rem_pio2_p(x, &y0, &y1, K);
     if (small) { y0 = x; y1 = 0.0; n = 0; }
     const double z = y0 * y0, w = z * z;
     const double r = sm_ksin_r(z, w, K);
