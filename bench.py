@@ -68,7 +68,12 @@ def pmc_profile(n, budget, chunk):
     configuration, if any: HBM traffic and fp64 VALU counts of k_rollout."""
     import glob
     best = None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json"))):
+    def order(path):   # tags r<round><letters>: r3h < r3z < r3aa < r3at (round, then length, then name)
+        tag = os.path.basename(path).split("_")[0]
+        rnd = int("".join(ch for ch in tag[1:] if ch.isdigit()) or 0)
+        return (rnd, len(tag), tag)
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")), key=order):
         try:
             s = json.load(open(path))
         except (OSError, ValueError):
