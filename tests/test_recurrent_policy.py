@@ -92,3 +92,27 @@ def test_configuration_checks():
                      policy_kwargs={"shared_lstm": True})
     with pytest.raises(ValueError):
         RecurrentPPO("MlpPolicy", env, n_steps=32, batch_size=64, seq_len=16)
+
+
+def test_pair_pass_and_split_weight_gradients_equal_per_network_autograd():
+    """The CPU form of the two-network pass (_run_pair: batched GEMMs, the input
+    projection with the bias folded in and its weight gradient summed over the
+    steps) against each LSTM run alone (_run): outputs bit for bit, parameter
+    gradients within float32 rounding."""
+    torch.manual_seed(3)
+    T, n, D, H = 8, 64, 10, 32
+    pol = RecurrentActorCritic(D, 3, lstm_hidden_size=H)
+    x = torch.randn(T, n, D)
+    state = torch.randn(4, n, H)
+    starts = (torch.rand(T, n) < 0.2).float()
+    w = torch.randn(T, n, H)
+    params = list(pol.lstm_actor.parameters()) + list(pol.lstm_critic.parameters())
+    lp, lv, new = pol.forward_seq(x, state, starts)
+    g1 = torch.autograd.grad((lp * w).sum() + (lv * w).sum() + new.sum(), params)
+    a, ha, ca = pol._run(pol.lstm_actor, x, state[0], state[1], starts)
+    v, hv, cv = pol._run(pol.lstm_critic, x, state[2], state[3], starts)
+    ref = torch.stack([ha, ca, hv, cv])
+    g0 = torch.autograd.grad((a * w).sum() + (v * w).sum() + ref.sum(), params)
+    assert torch.equal(lp, a) and torch.equal(lv, v) and torch.equal(new, ref)
+    for p, q in zip(g1, g0):
+        assert torch.allclose(p, q, rtol=1e-4, atol=1e-5)
