@@ -36,7 +36,7 @@ import torch
 from torch import nn
 
 from . import _lib
-from .ppo import PPO, SplitKLinear, _ortho, allreduce_gradients
+from .ppo import PPO, SplitKLinear, _ortho, allreduce_gradients, ppo_loss
 
 __all__ = ["RecurrentActorCritic", "RecurrentPPO", "lstm_cell"]
 
@@ -371,23 +371,35 @@ class RecurrentPPO(PPO):
         obs, act = b.obs[t, ee], b.actions[t, ee]
         old_lp, adv, ret, starts = b.log_probs[t, ee], b.advantages[t, ee], b.returns[t, ee], b.episode_starts[t, ee]
         state = self.seq_states[k, :, e].transpose(0, 1)                             # [4, m, H]
-        v, lp, ent = pol.evaluate(obs, act, state, starts)
-        v, lp, ent, old_lp, adv, ret = (x.reshape(-1) for x in (v, lp, ent, old_lp, adv, ret))
-        if self.normalize_advantage and adv.numel() > 1:
-            adv = (adv - adv.mean()) / (adv.std() + 1e-8)
-        ratio = torch.exp(lp - old_lp)
+        old_lp, adv, ret = (x.reshape(-1) for x in (old_lp, adv, ret))
+        norm = self.normalize_advantage and adv.numel() > 1
         cr = self._clip()
-        pg = -torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - cr, 1 + cr)).mean()
-        vf = torch.nn.functional.mse_loss(ret, v)
-        ent_loss = -ent.mean()
-        loss = pg + self.ent_coef * ent_loss + self.vf_coef * vf
+        if obs.is_cuda:
+            # the loss head as the fused HIP kernels of salp_ppo_loss (the MLP
+            # PPO's, ppo.ppo_loss): one launch each way instead of ~25
+            lat_pi, lat_vf, _ = pol.forward_seq(obs, state, starts)
+            mean = pol.action_net(pol.pi_net(lat_pi.reshape(-1, lat_pi.shape[-1])))
+            value = pol.value_net(pol.vf_net(lat_vf.reshape(-1, lat_vf.shape[-1]))).reshape(-1)
+            loss, stats = ppo_loss(mean, pol.log_std, value, act.reshape(-1, act.shape[-1]), old_lp, adv, ret, cr,
+                                   self.ent_coef, self.vf_coef, norm)
+        else:
+            v, lp, ent = pol.evaluate(obs, act, state, starts)
+            v, lp, ent = (x.reshape(-1) for x in (v, lp, ent))
+            if norm:
+                adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+            ratio = torch.exp(lp - old_lp)
+            pg = -torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - cr, 1 + cr)).mean()
+            vf = torch.nn.functional.mse_loss(ret, v)
+            ent_loss = -ent.mean()
+            loss = pg + self.ent_coef * ent_loss + self.vf_coef * vf
+            clip = ((ratio - 1).abs() > cr).float().mean()
+            stats = torch.stack([pg.detach(), vf.detach(), -ent_loss.detach(), clip.detach()])
         self.opt.zero_grad(set_to_none=False)
         loss.backward()
         allreduce_gradients(list(pol.parameters()))
         nn.utils.clip_grad_norm_(pol.parameters(), self.max_grad_norm)
         self.opt.step()
-        clip = ((ratio - 1).abs() > cr).float().mean()
-        acc += torch.stack([pg.detach(), vf.detach(), -ent_loss.detach(), clip.detach()])
+        acc += stats
 
     def _minibatch(self, idx, acc):
         # PPO._graphed_minibatch captures / replays this with `idx` = sequence ids
