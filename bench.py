@@ -65,9 +65,16 @@ HOT_FIELDS = slice(FIELD["v0"], FIELD["ang2"] + 1)   # kinematic state: NaN once
 
 def pmc_profile(n, budget, chunk):
     """The committed PMC summary (tools/pmc_summary.py) measured on this exact
-    configuration, if any: HBM traffic and fp64 VALU counts of k_rollout."""
+    configuration AND on this exact k_rollout machine code, if any: HBM
+    traffic and fp64 VALU counts.  Returns (name, summary, None) or (None, None,
+    reason): a summary whose kernel fingerprint differs from the library's is
+    stale and is not reported as measured."""
     import glob
+    from grasp_lab_salp_amd import _codeobj
+    from grasp_lab_salp_amd._lib import LIB_PATH
+    sha = _codeobj.kernel_sha(LIB_PATH, _codeobj.ROLLOUT_KERNEL)
     best = None
+    stale = []
     def order(path):   # tags r<round><letters>: r3h < r3z < r3aa < r3at (round, then length, then name)
         tag = os.path.basename(path).split("_")[0]
         rnd = int("".join(ch for ch in tag[1:] if ch.isdigit()) or 0)
@@ -83,7 +90,14 @@ def pmc_profile(n, budget, chunk):
         d = s.get("derived", {})
         if (s.get("config") == {"n_envs": n, "tick_budget": budget, "chunk": chunk}
                 and d.get("hbm_bytes") and d.get("fp64_flops")):
-            best = (os.path.basename(path), s)
+            if s.get("kernel_sha16") == sha:
+                best = (os.path.basename(path), s, None)
+            else:
+                stale.append(os.path.basename(path))
+    if best is None:
+        why = (f"no PMC summary of this config was measured on this k_rollout build (kernel_sha16 {sha}); "
+               f"stale summaries: {stale[-3:]}" if stale else "no PMC summary of this config")
+        return None, None, why
     return best
 
 
@@ -415,6 +429,9 @@ def main(argv=None):
         return
 
     prof = pmc_profile(n, a.tick_budget, a.chunk)
+    from grasp_lab_salp_amd import _codeobj
+    from grasp_lab_salp_amd._lib import LIB_PATH
+    kernel_sha = _codeobj.kernel_sha(LIB_PATH, _codeobj.ROLLOUT_KERNEL)
     budget_ticks = float(-(-a.tick_budget // a.chunk) * a.chunk) * n * a.steps * world
     steps_per_launch = steps_local / a.steps
     bytes_launch = steps_per_launch * BYTES_PER_ENV_STEP
@@ -448,8 +465,9 @@ def main(argv=None):
         "kernel_ms_per_launch": kern_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": prof[1]["derived"].get("hbm_bytes") if prof else None,
-                     "traffic_source": prof[0] if prof else None,
+                     "traffic": prof[1]["derived"].get("hbm_bytes") if prof[1] else None,
+                     "traffic_source": prof[0] if prof[1] else prof[2],
+                     "kernel_sha16": kernel_sha,
                      "bytes_per_launch": bytes_launch,
                      "bytes_per_env_step": BYTES_PER_ENV_STEP,
                      "note": "algorithmic bytes = env-steps per launch x (2 x 816 B state + 97 B outputs) "
@@ -471,7 +489,7 @@ def main(argv=None):
     res["roofline_valu"] = {"bound": "fp64-valu", "achieved": fl_algo, "peak": FP64_VALU_PEAK_TFLOPS,
                             "unit": "TFLOP/s", "frac": fl_algo / FP64_VALU_PEAK_TFLOPS,
                             "flops_per_env_tick": F_TICK_ALGO, "count": "algorithmic (DESIGN.md §5)"}
-    if prof:
+    if prof[1]:
         d = prof[1]["derived"]
         per = prof[1]["per_dispatch"]
         if d.get("fp64_flops"):
@@ -490,8 +508,13 @@ def main(argv=None):
         res["parity_sampled"] = parity
     if ppo is not None:
         res["ppo"] = ppo
-    if world == 1 and not a.no_cpu_baseline:
+    if not a.no_cpu_baseline:
+        # rank 0, after every rank's timed region (the other ranks have left):
+        # the same bounded oracle sample at every N, on rank 0's CPU share
         res["cpu_baseline"] = cpu_baseline(a.cpu_baseline_seconds)
+        if world > 1:
+            res["cpu_baseline"]["note"] += (f"; measured on rank 0 after the {world}-rank timed region, "
+                                            f"with rank 0's CPU share ({res['cpu_baseline']['cores']} threads)")
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -132,12 +132,34 @@ class BatchedSalpEnv:
                                               _ptr(obs), self._stream()))
         return obs
 
-    def step(self, actions, auto_reset=False, want_terminal_obs=True):
+    def step(self, actions, auto_reset=False, want_terminal_obs=True, out=None):
         """One env.step per env. actions [n,3] float32 in Box([0,0,-1],[1,1,1]).
 
         Returns a :class:`StepResult`; ``info`` is an [n, INFO_DIM] fp64 tensor
-        (columns ``_abi.INFO_KEYS``; see :meth:`info_dicts`)."""
+        (columns ``_abi.INFO_KEYS``; see :meth:`info_dicts`).  ``out``: a dict of
+        preallocated contiguous device tensors to write into instead ("obs" [n,
+        obs_dim] f32, "reward" [n] f64, "terminated" / "truncated" [n] u8,
+        "terminal_obs" [n, obs_dim] f32 or None, "info" [n, INFO_DIM] f64 or
+        None); the result then holds those tensors (flags as u8)."""
         a = self._f32(actions, (self.n_envs, 3))
+        if out is not None:
+            n, od = self.n_envs, self.obs_dim
+            want = {"obs": ((n, od), torch.float32), "reward": ((n,), torch.float64),
+                    "terminated": ((n,), torch.uint8), "truncated": ((n,), torch.uint8),
+                    "terminal_obs": ((n, od), torch.float32), "info": ((n, INFO_DIM), torch.float64)}
+            for k, (shape, dt) in want.items():
+                t = out.get(k)
+                if t is None and k in ("terminal_obs", "info"):
+                    continue
+                if (t is None or tuple(t.shape) != shape or t.dtype != dt or not t.is_contiguous()
+                        or t.device != self.device):
+                    raise ValueError(f"step(out=...): {k!r} must be a contiguous {dt} tensor of shape {shape} "
+                                     f"on {self.device}")
+            obs, rew, term, trunc = out["obs"], out["reward"], out["terminated"], out["truncated"]
+            tobs, info = out.get("terminal_obs"), out.get("info")
+            self._run(_lib.load().salp_step(self._h, _ptr(a), _ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc),
+                                              int(bool(auto_reset)), _ptr(tobs), _ptr(info), self._stream()))
+            return StepResult(obs, rew, term, trunc, tobs, info)
         obs = torch.empty((self.n_envs, self.obs_dim), dtype=torch.float32, device=self.device)
         rew = torch.empty(self.n_envs, dtype=torch.float64, device=self.device)
         term = torch.empty(self.n_envs, dtype=torch.uint8, device=self.device)

@@ -352,7 +352,7 @@ class PPO:
     def __init__(self, policy, env, learning_rate=3e-4, n_steps=2048, batch_size=64, n_epochs=10, gamma=0.99,
                  gae_lambda=0.95, clip_range=0.2, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5,
                  normalize_advantage=True, seed=0, device=None, verbose=0, reset_nonfinite=True,
-                 use_graphs=None, fused_loss=None, collect="auto", fused_update=None):
+                 use_graphs=None, fused_loss=None, collect="auto", fused_update=None, max_graph_minibatches=1024):
         if policy not in ("MlpPolicy", None) and not isinstance(policy, nn.Module):
             raise ValueError("policy must be 'MlpPolicy' or an nn.Module")
         if fused_loss and isinstance(policy, nn.Module) and not all(
@@ -382,6 +382,8 @@ class PPO:
         # built-in policy on a GPU; torch ops + torch Adam otherwise
         if fused_update and not isinstance(self.policy, ActorCritic):
             raise ValueError("fused_update=True runs the built-in ActorCritic (64-64 tanh MlpPolicy) only")
+        if fused_update and self.device.type != "cuda":
+            raise ValueError("fused_update=True runs HIP kernels: it needs a ROCm GPU device")
         self.fused_update = (self.device.type == "cuda" and isinstance(self.policy, ActorCritic)
                              and self.policy.pi_net[0].out_features == 64 if fused_update is None
                              else bool(fused_update))
@@ -397,9 +399,11 @@ class PPO:
                                     capturable=self.use_graphs, fused=fused or None)
         self._graph = None
         self._graph_warm = 0
-        self._epoch_graph = None   # fused step, one GPU: one graph per epoch of minibatches
+        self._epoch_graph = None   # fused step, one GPU: one graph per chunk of minibatches
+        self.max_graph_minibatches = max(1, int(max_graph_minibatches))
         self._g_clip = None
         self._collect_stream = None
+        self._train_stream = None
         self.n_steps, self.batch_size, self.n_epochs = int(n_steps), int(batch_size), int(n_epochs)
         # clip_range may be an SB3-style schedule: f(progress_remaining) -> value
         self.gamma, self.gae_lambda, self.clip_range = gamma, gae_lambda, clip_range
@@ -671,8 +675,11 @@ class PPO:
         buffers; Adam is capturable).  The fused step allocates nothing and
         reads only persistent buffers: it is captured on its first call and
         the graph is kept across updates."""
-        if self._graph is not None and self.fused_update and self._g_clip != self._clip():
-            self._graph = None   # a clip_range schedule moved: the captured value is stale
+        if self._graph is not None and self._g_clip != self._clip():
+            # a clip_range schedule moved: the value captured in the graph is
+            # stale (fused and torch steps alike; the torch step's warm-up is
+            # done, so it recaptures at once)
+            self._graph = None
         if self._graph is None and self.fused_update:
             if self._graph_warm == 0:
                 self._g_idx = torch.empty_like(idx)
@@ -705,6 +712,7 @@ class PPO:
                 self._graph_warm += 1
                 return
             self.opt.zero_grad(set_to_none=True)
+            self._g_clip = self._clip()
             self._graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self._graph, capture_error_mode=_CAPTURE_MODE):
                 self._minibatch(self._g_idx, self._g_acc)
@@ -749,33 +757,54 @@ class PPO:
         vals = (acc / max(steps, 1)).tolist()
         return dict(zip(("pg_loss", "vf_loss", "entropy", "clip_frac"), vals))
 
+    def _graph_chunk(self, m):
+        """Minibatches per captured graph: the largest divisor of the epoch's
+        `m` minibatches that is at most max_graph_minibatches (a graph's node
+        count and its capture loop stay bounded whatever n_steps x n_envs /
+        batch_size is: SB3's default batch_size 64 at 32 768 envs x 2 048 steps
+        would otherwise be a million minibatches in one graph)."""
+        cap = min(m, self.max_graph_minibatches)
+        return max(d for d in range(1, cap + 1) if m % d == 0)
+
     def _train_epoch_graphs(self):
-        """train() for the fused step on one GPU: every minibatch of an epoch
-        reads its rows from a slice of one persistent permutation, so the whole
-        epoch (4 kernels per minibatch) is one HIP graph, captured once and
-        replayed n_epochs times per update after a fresh permutation is drawn
-        into it.  The same kernels in the same order as minibatch by minibatch
-        (no per-minibatch index copy, no per-minibatch launch from Python)."""
+        """train() for the fused step on one GPU: every minibatch reads its rows
+        from a slice of one persistent index buffer, so a chunk of C
+        minibatches (4 kernels each) is one HIP graph, captured once and
+        replayed M / C times per epoch (M minibatches per epoch; C = M, one
+        graph per epoch, unless M exceeds max_graph_minibatches), each time
+        after the next C x batch_size indices of the epoch's permutation are
+        copied into it.  The same kernels in the same order as minibatch by
+        minibatch (no per-minibatch launch from Python)."""
         N = self.n_steps * self.n_envs
         bs = self.batch_size
+        m = N // bs
+        c = self._graph_chunk(m)
         fresh = False
         if self._epoch_graph is None or self._g_clip != self._clip():
             if self._epoch_graph is None:
                 self._perm = torch.empty(N, dtype=torch.int64, device=self.device)
+                # the graph's index buffer: the permutation itself when one
+                # graph covers the epoch, else a chunk-sized copy target
+                self._gperm = self._perm if c == m else torch.empty(c * bs, dtype=torch.int64, device=self.device)
                 self._g_acc = torch.zeros(4, device=self.device)
             torch.randperm(N, generator=self.gen, device=self.device, out=self._perm)
+            if c != m:
+                self._gperm.copy_(self._perm[:c * bs])
             self._g_clip = self._clip()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
-                for s in range(0, N, bs):
-                    self._fused_minibatch(self._perm[s:s + bs], self._g_acc)
+                for s in range(0, c * bs, bs):
+                    self._fused_minibatch(self._gperm[s:s + bs], self._g_acc)
             self._epoch_graph = g
             fresh = True
         for e in range(self.n_epochs):
             if not (fresh and e == 0):   # the capture's permutation serves the first epoch
                 torch.randperm(N, generator=self.gen, device=self.device, out=self._perm)
-            self._epoch_graph.replay()
-        vals = (self._g_acc / (self.n_epochs * (N // bs))).tolist()
+            for k in range(m // c):
+                if c != m and not (fresh and e == 0 and k == 0):
+                    self._gperm.copy_(self._perm[k * c * bs:(k + 1) * c * bs])
+                self._epoch_graph.replay()
+        vals = (self._g_acc / (self.n_epochs * m)).tolist()
         self._g_acc.zero_()
         return dict(zip(("pg_loss", "vf_loss", "entropy", "clip_frac"), vals))
 
@@ -789,6 +818,7 @@ class PPO:
         stream = torch.cuda.current_stream(self.device)
         if self._collect_stream is None and self.device.type == "cuda":
             self._collect_stream = torch.cuda.Stream(self.device)
+            self._train_stream = torch.cuda.Stream(self.device)
         while self.num_timesteps < total_timesteps:
             done_frac = (self.num_timesteps - start_steps) / max(total_timesteps - start_steps, 1)
             self._progress = 1.0 - done_frac
@@ -803,7 +833,18 @@ class PPO:
                 stream.wait_stream(cs)
             else:
                 ev = self.collect_rollouts()
-            self.logger = self.train()
+            if self._train_stream is not None:
+                # the update (warm-up, captures and replays) on a stream the
+                # learner owns: eager work a caller issues between learn()
+                # calls (predict, an evaluation loop) never lands on the
+                # stream the kept graphs replay on
+                ts = self._train_stream
+                ts.wait_stream(stream)
+                with torch.cuda.stream(ts):
+                    self.logger = self.train()
+                stream.wait_stream(ts)
+            else:
+                self.logger = self.train()
             end = torch.cuda.Event(enable_timing=True)
             end.record(stream)
             end.synchronize()

@@ -25,7 +25,7 @@ from typing import Dict, Optional, Tuple
 import numpy as np
 import torch
 
-from ._abi import EPISODE_METRIC_KEYS, INFO, MAX_OBSTACLES, REWARD_COMPONENT_KEYS
+from ._abi import EPISODE_METRIC_KEYS, FIELD, INFO, MAX_OBSTACLES, REWARD_COMPONENT_KEYS
 from .batched_env import BatchedSalpEnv
 from .robot import Robot
 from .spaces import Box, GymEnv
@@ -110,7 +110,8 @@ class SalpRobotEnv(GymEnv):
         self.target_radius = TARGET_RADIUS
         self.num_obstacles = num_obstacles
         self.obstacle_radius = obstacle_radius
-        self.obstacles = []
+        self._obstacles = []
+        self._target_point = None
         self.render_mode = render_mode
         self.action_randomization = False
         self.observation_randomization = False
@@ -153,14 +154,72 @@ class SalpRobotEnv(GymEnv):
         self._sim.set_randomization(self.robot.dynamics_randomization, self.robot.disturbances,
                                     self.action_randomization, self.observation_randomization, self.latency)
 
+    # ------------------------------------------------------------ task attributes
+    # Plain attributes in the reference, read by its own step() every cycle
+    # (src/salp_robot_env.py:349-397, 561-568, 651-670).  Assigning one between
+    # steps - placing a target or obstacles by hand, as the edge-case episodes
+    # of tests/golden/make_golden.py do - changes what the next step computes,
+    # so here the setters write the value through to the env's device state.
+    # The observation is recomputed by the next step() / reset().
+    @property
+    def target_point(self):
+        return self._target_point
+
+    @target_point.setter
+    def target_point(self, value):
+        self._target_point = value
+        v = np.asarray(value, dtype=np.float64).reshape(-1)
+        self._write_fields({"target0": v[0], "target1": v[1]})
+
+    @property
+    def obstacles(self):
+        return self._obstacles
+
+    @obstacles.setter
+    def obstacles(self, value):
+        value = list(value)
+        if len(value) > self.num_obstacles:
+            raise ValueError(f"at most num_obstacles = {self.num_obstacles} obstacles (observation size)")
+        self._obstacles = value
+        vals = {"n_obst": float(len(value))}
+        for k in range(MAX_OBSTACLES):
+            o = np.asarray(value[k], dtype=np.float64).reshape(-1) if k < len(value) else np.zeros(2)
+            vals[f"obst{2 * k}"], vals[f"obst{2 * k + 1}"] = o[0], o[1]
+        self._write_fields(vals)
+
+    @property
+    def prev_dist(self):
+        return float(self._sim.field("prev_dist")[0])
+
+    @prev_dist.setter
+    def prev_dist(self, value):
+        self._write_fields({"prev_dist": value})
+
+    @property
+    def initial_target_distance(self):
+        return float(self._sim.field("init_dist")[0])
+
+    @initial_target_distance.setter
+    def initial_target_distance(self, value):
+        self._write_fields({"init_dist": value})
+
+    def _write_fields(self, values):
+        sim = getattr(self, "_sim", None)
+        if sim is None:   # during __init__, before the device env exists
+            return
+        st = sim.get_state()
+        for name, v in values.items():
+            st[FIELD[name], 0] = float(v)
+        sim.set_state(st)
+
     # ------------------------------------------------------------ helpers
     def generate_target_point(self, strategy: str = "random", center=None, max_distance: float = 2.0):
         cur = self.robot.position_world[:2] if self.robot._bound else None
         return draw_target(self.width, self.height, strategy, cur, center, max_distance)
 
     def _generate_obstacles(self):
-        self.obstacles = draw_obstacles(self.width, self.height, self.num_obstacles,
-                                        self.obstacle_radius, self.target_point)
+        self._obstacles = draw_obstacles(self.width, self.height, self.num_obstacles,
+                                         self.obstacle_radius, self.target_point)
 
     @staticmethod
     def _rescale_action(action):
@@ -198,7 +257,8 @@ class SalpRobotEnv(GymEnv):
         seeds self.np_random; targets and obstacles come from np.random."""
         if seed is not None:
             self.np_random = np.random.default_rng(seed)
-        self.target_point = self.generate_target_point(strategy="random")
+        # drawn on the host, handed to the device by reset_to below
+        self._target_point = self.generate_target_point(strategy="random")
         self._generate_obstacles()
         ob = np.zeros((1, MAX_OBSTACLES, 2), np.float32)
         for k, o in enumerate(self.obstacles):

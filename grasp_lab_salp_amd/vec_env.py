@@ -28,9 +28,16 @@ obstacle placement fails the observation keeps its length with zeros in the
 missing slots (the reference returns a shorter vector).
 
 For throughput, :meth:`SalpVecEnv.step_tensors` returns device tensors and
-builds no Python dicts.
+builds no Python dicts.  ``step_wait`` moves every output of a step to the host
+in ONE copy (a packed device buffer into one of two pinned host buffers) and
+returns the infos as a :class:`StepInfos` sequence whose per-env dicts are built
+when they are first read: the reference's own consumer
+(src/tensorboard_callback.py:72-123) reads the infos of the envs that finished,
+so 65 536 reward-component dicts per step are never built unless asked for.
 """
+import collections.abc
 import time
+import weakref
 
 import numpy as np
 import torch
@@ -60,7 +67,127 @@ except ImportError:  # pragma: no cover
         def unwrapped(self):
             return self
 
-__all__ = ["SalpVecEnv", "make_vec_env"]
+__all__ = ["SalpVecEnv", "StepInfos", "make_vec_env"]
+
+
+_COMP_COLS = [INFO[k] for k in REWARD_COMPONENT_KEYS]
+_METRIC_COLS = [(k, INFO[k]) for k in EPISODE_METRIC_KEYS]
+
+
+class StepInfos(collections.abc.Sequence):
+    """The ``infos`` list of one :meth:`SalpVecEnv.step_wait`, built on access.
+
+    ``infos[i]`` is the dict the reference env (wrapped in SB3's Monitor,
+    auto-reset by the VecEnv) returns for env i: its reward components
+    (src/salp_robot_env.py:279-289) and, when env i finished, ``terminal_observation``,
+    ``TimeLimit.truncated``, ``episode`` {"r", "l", "t"} and the episode metrics
+    (:399-447).  A dict is built the first time it is read and then kept (a
+    consumer's edits stick).  ``done_indices`` lists the envs that finished.
+    Values come from the step's host copy; the VecEnv detaches them (private
+    copies) before it reuses that pinned buffer, so a kept StepInfos stays valid."""
+
+    __slots__ = ("_info", "_tobs", "_term", "_trunc", "_done", "_t", "_cache", "__weakref__")
+
+    def __init__(self, info, tobs, term, trunc, done, t):
+        self._info, self._tobs, self._term, self._trunc, self._done, self._t = info, tobs, term, trunc, done, t
+        self._cache = {}
+
+    def __len__(self):
+        return len(self._done)
+
+    @property
+    def done_indices(self):
+        return np.nonzero(self._done)[0]
+
+    def _build(self, i):
+        row = self._info[i]
+        d = dict(zip(REWARD_COMPONENT_KEYS, row[_COMP_COLS].tolist()))
+        if self._done[i]:
+            d["terminal_observation"] = np.array(self._tobs[i])
+            d["TimeLimit.truncated"] = bool(self._trunc[i] and not self._term[i])
+            d["episode"] = {"r": round(float(row[INFO["ep_return"]]), 6), "l": int(row[INFO["ep_len"]]),
+                            "t": self._t}
+            d.update({k: float(row[c]) for k, c in _METRIC_COLS})
+        return d
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        i = int(i)
+        if i < 0:
+            i += len(self)
+        if not 0 <= i < len(self):
+            raise IndexError("env index out of range")
+        d = self._cache.get(i)
+        if d is None:
+            d = self._cache[i] = self._build(i)
+        return d
+
+    def __iter__(self):
+        for i in range(len(self)):
+            yield self[i]
+
+    def _detach(self):
+        """Private copies of the arrays still read from the shared pinned buffer."""
+        self._info = np.array(self._info)
+        self._tobs = np.array(self._tobs)
+        self._term = np.array(self._term)
+        self._trunc = np.array(self._trunc)
+
+
+class _EmptyInfos(StepInfos):
+    """``infos=False``: an empty dict per env (built on access, kept)."""
+
+    __slots__ = ()
+
+    def _build(self, i):
+        return {}
+
+
+class _HostStage:
+    """One packed device buffer that salp_step writes into (info f64 [n, INFO_DIM],
+    reward f64 [n], obs and terminal obs f32 [n, obs_dim], terminated /
+    truncated u8 [n]) and two pinned host buffers it is copied to in turn."""
+
+    def __init__(self, n, od, device, with_info):
+        parts = [("info", (n, len(INFO)), torch.float64, with_info), ("reward", (n,), torch.float64, True),
+                 ("obs", (n, od), torch.float32, True), ("terminal_obs", (n, od), torch.float32, with_info),
+                 ("terminated", (n,), torch.uint8, True), ("truncated", (n,), torch.uint8, True)]
+        self.layout, off = [], 0
+        for name, shape, dt, on in parts:
+            if not on:
+                continue
+            nb = int(np.prod(shape)) * torch.empty((), dtype=dt).element_size()
+            self.layout.append((name, off, shape, dt))
+            off += (nb + 63) // 64 * 64
+        self.nbytes = off
+        self.dev = torch.empty(off, dtype=torch.uint8, device=device)
+        self.host = [torch.empty(off, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+        self.holders = [None, None]   # weakrefs to the StepInfos reading each host buffer
+        self.k = 0
+
+    @staticmethod
+    def _views(buf, layout):
+        out = {}
+        for name, off, shape, dt in layout:
+            nb = int(np.prod(shape)) * torch.empty((), dtype=dt).element_size()
+            out[name] = buf[off:off + nb].view(dt).view(shape)
+        return out
+
+    def device_out(self):
+        return self._views(self.dev, self.layout)
+
+    def download(self, stream):
+        """Copy the packed buffer to the next host buffer; numpy views of it."""
+        k = self.k
+        self.k ^= 1
+        old = self.holders[k]() if self.holders[k] is not None else None
+        if old is not None:
+            old._detach()
+        self.holders[k] = None
+        self.host[k].copy_(self.dev, non_blocking=True)
+        stream.synchronize()
+        return k, {name: v.numpy() for name, v in self._views(self.host[k], self.layout).items()}
 
 
 class SalpVecEnv(_VecEnvBase):
@@ -82,6 +209,7 @@ class SalpVecEnv(_VecEnvBase):
         self.build_infos = bool(infos)
         self._actions = None
         self._t0 = time.time()
+        self._stage = None
 
     # ------------------------------------------------------------- VecEnv
     def reset(self):
@@ -98,35 +226,29 @@ class SalpVecEnv(_VecEnvBase):
         return self.sim.step(actions, auto_reset=True, want_terminal_obs=True)
 
     def step_wait(self):
+        """SB3 ``step_wait``: one salp_step with auto-reset into a packed device
+        buffer, ONE device-to-host copy of it (pinned), then fresh NumPy obs /
+        float32 rewards / bool dones and a lazy :class:`StepInfos` (SB3's
+        ``TimeLimit.truncated``, ``terminal_observation`` and Monitor ``episode``
+        on the envs that finished; ``infos=False``: empty dicts)."""
         a = self._actions
         if not torch.is_tensor(a):
             a = torch.as_tensor(np.asarray(a, np.float32))
-        r = self.step_tensors(a)
-        obs = r.obs.cpu().numpy()
-        rew = r.reward.float().cpu().numpy()
-        term = r.terminated.cpu().numpy()
-        trunc = r.truncated.cpu().numpy()
+        if self._stage is None:
+            self._stage = _HostStage(self.num_envs, self.sim.obs_dim, self.sim.device, self.build_infos)
+        st = self._stage
+        self.sim.step(a, auto_reset=True, out=st.device_out())
+        k, h = st.download(torch.cuda.current_stream(self.sim.device))
+        obs = np.array(h["obs"])
+        rew = h["reward"].astype(np.float32)
+        term, trunc = h["terminated"] != 0, h["truncated"] != 0
         dones = term | trunc
-        infos = self._infos(r, term, trunc, dones) if self.build_infos else [{} for _ in range(self.num_envs)]
+        if self.build_infos:
+            infos = StepInfos(h["info"], h["terminal_obs"], term, trunc, dones, round(time.time() - self._t0, 6))
+            st.holders[k] = weakref.ref(infos)
+        else:
+            infos = _EmptyInfos(None, None, term, trunc, dones, 0.0)
         return obs, rew, dones, infos
-
-    def _infos(self, r, term, trunc, dones):
-        info = r.info.cpu().numpy()
-        comp = info[:, [INFO[k] for k in REWARD_COMPONENT_KEYS]].tolist()
-        out = [dict(zip(REWARD_COMPONENT_KEYS, c)) for c in comp]
-        idx = np.nonzero(dones)[0]
-        if len(idx):
-            tobs = r.terminal_obs[torch.as_tensor(idx, device=r.terminal_obs.device)].cpu().numpy()
-            t = round(time.time() - self._t0, 6)
-            for j, i in enumerate(idx):
-                row = info[i]
-                d = out[i]
-                d["terminal_observation"] = tobs[j]
-                d["TimeLimit.truncated"] = bool(trunc[i] and not term[i])
-                d["episode"] = {"r": round(float(row[INFO["ep_return"]]), 6),
-                                "l": int(row[INFO["ep_len"]]), "t": t}
-                d.update({k: float(row[INFO[k]]) for k in EPISODE_METRIC_KEYS})
-        return out
 
     def close(self):
         self.sim.close()

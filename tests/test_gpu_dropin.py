@@ -147,12 +147,20 @@ def _make_env(**kw):
     return SalpRobotEnv(render_mode=None, robot=robot, **kw)
 
 
-@pytest.mark.parametrize("job", [0, 3, 17, 21, 22])
+# tests/golden/make_golden.py build_jobs(): jobs 19 and 20 place the target and
+# obstacles by hand after reset (edge cases: a target near an obstacle, a target
+# 0.25 m away), the others draw them from np.random
+INJECT = {19: ([1.9, 0.0], [[0.45, 0.0], [0.0, 1.2]]), 20: ([0.25, 0.0], [[1.0, 1.0], [1.5, -1.0]])}
+
+
+@pytest.mark.parametrize("job", list(range(23)))
 def test_salp_robot_env_reproduces_reference_episodes(job):
     """make_env + np.random.seed(seed) + reset + the fixture's actions: the
     drop-in env redraws the reference's targets/obstacles itself and must
     follow the reference's episode (obs 1e-5 relative, same flags) — the
-    whole episode free-running, resets included."""
+    whole episode free-running, resets included.  Every fixture episode: the
+    fixed-action one, 16 random ones, the 503-step scripted one, the two with
+    a hand-placed target and obstacles, and the 0- and 4-obstacle envs."""
     d = load_episodes()
     rows = np.where(d["job_index"] == job)[0]
     K = int(d["num_obstacles_cfg"][rows[0]])
@@ -161,6 +169,13 @@ def test_salp_robot_env_reproduces_reference_episodes(job):
     env = _make_env(num_obstacles=K)
     obs, info = env.reset()
     assert info == {}
+    if job in INJECT:
+        # the reference script's own assignments (make_golden.py run_episode_job)
+        tgt, obst = INJECT[job]
+        env.target_point = np.asarray(tgt, np.float32)
+        env.obstacles = [np.asarray(o, np.float32) for o in obst]
+        env.prev_dist = np.linalg.norm(env.robot.position_world[0:-1] - env.target_point)
+        env.initial_target_distance = env.prev_dist
     assert np.array_equal(env.target_point, d["b_e_target"][rows[0]])
     od = 6 + 2 * K
     for r in rows:
@@ -260,6 +275,31 @@ def test_vec_env_semantics_against_oracle():
         for i in np.nonzero(~dones)[0][:5]:
             assert "episode" not in infos[i] and "rewards/track" in infos[i]
     assert seen_done > 0
+
+
+def test_vec_env_infos_stay_valid_after_later_steps():
+    """step_wait's infos read the step's pinned host copy lazily; two pinned
+    buffers alternate and a StepInfos still alive when its buffer is reused is
+    detached first, so infos read after later steps hold their own step's values."""
+    n = 512
+    venv = SalpVecEnv(n, seed=9)
+    venv.reset()
+    rng = np.random.default_rng(4)
+    kept, snaps = [], []
+    for t in range(6):
+        a = np.stack([rng.uniform(0, 1, n), rng.uniform(0, 0.3, n), rng.uniform(-1, 1, n)], 1).astype(np.float32)
+        _, _, dones, infos = venv.step(a)
+        kept.append((infos, dones.copy()))
+        snaps.append((np.array(infos._info), np.array(infos._tobs)))
+    for (infos, dones), (info, tobs) in zip(kept, snaps):
+        for i in list(np.nonzero(dones)[0][:8]) + [0, n - 1]:
+            d = infos[i]
+            assert d["rewards/track"] == info[i, INFO["rewards/track"]]
+            if dones[i]:
+                assert np.array_equal(d["terminal_observation"], tobs[i], equal_nan=True)
+                assert d["episode"]["l"] == int(info[i, INFO["ep_len"]])
+        assert list(infos.done_indices) == list(np.nonzero(dones)[0])
+    venv.close()
 
 
 def test_make_vec_env_from_reference_make_env():

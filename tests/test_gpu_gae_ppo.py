@@ -288,3 +288,82 @@ def test_graphed_update_matches_eager_after_several_collections():
     assert all(torch.isfinite(p).all() for p in model.policy.parameters())
     assert all(r["vf_loss"] == r["vf_loss"] for r in model.history)
     env.close()
+
+
+def _graph_vs_eager_checker(model):
+    """Wrap model._graphed_minibatch: at the first graphed minibatch of every
+    update from the second on, replay the graph, then rerun the same minibatch
+    eagerly from the same parameters / Adam state and record whether the
+    gradients agree bit for bit (the graph's results are kept)."""
+    seen, graphs = {}, []
+    inner = model._graphed_minibatch
+
+    def tensors():
+        out = []
+        for p in model.policy.parameters():
+            out.append(p.data)
+            out += [v for v in model.opt.state.get(p, {}).values() if torch.is_tensor(v)]
+        return out
+
+    def check(idx):
+        upd = len(model.history) + 1
+        if upd < 2 or upd in seen:
+            return inner(idx)
+        pre = [t.clone() for t in tensors()]
+        inner(idx)
+        graphs.append(id(model._graph))
+        g_graph = [p.grad.clone() for p in model.policy.parameters()]
+        post = [t.clone() for t in tensors()]
+        keep = [p.grad for p in model.policy.parameters()]
+        for t, s in zip(tensors(), pre):
+            t.copy_(s)
+        for p in model.policy.parameters():
+            p.grad = None
+        model._minibatch(model._g_idx, torch.zeros(4, device=model.device))
+        seen[upd] = all(torch.equal(a, p.grad) for a, p in zip(g_graph, model.policy.parameters()))
+        for p, g in zip(model.policy.parameters(), keep):
+            p.grad = g
+        for t, s in zip(tensors(), post):
+            t.copy_(s)
+
+    model._graphed_minibatch = check
+    return seen, graphs
+
+
+def test_torch_graph_follows_a_clip_range_schedule():
+    """the torch-step graph bakes clip_range in as a constant; with
+    an SB3-style callable schedule it is recaptured whenever the value moves,
+    so every update's graphed step equals the eager step at that update's clip."""
+    from grasp_lab_salp_amd.ppo import PPO
+    from grasp_lab_salp_amd.vec_env import SalpVecEnv
+    env = SalpVecEnv(4096, seed=2, infos=False)
+    model = PPO("MlpPolicy", env, n_steps=16, batch_size=4096, n_epochs=4, seed=0, use_graphs=True,
+                fused_update=False, collect="lockstep", clip_range=lambda progress: 0.05 + 0.25 * progress)
+    seen, graphs = _graph_vs_eager_checker(model)
+    model.learn(4 * 16 * 4096)
+    assert sorted(seen) == [2, 3, 4] and all(seen.values()), seen
+    assert len(set(graphs)) == 3, "one capture per clip value"
+    env.close()
+
+
+def test_eager_forward_between_learn_calls_leaves_the_kept_graph_exact():
+    """the update runs on a stream the learner owns, so an eager
+    policy forward on the default stream between two learn() calls (predict,
+    an evaluation loop) cannot leave the kept torch-step graph reading a stale
+    BLAS workspace: graphed == eager in updates 2-4, one graph."""
+    from grasp_lab_salp_amd.ppo import PPO
+    from grasp_lab_salp_amd.vec_env import SalpVecEnv
+    env = SalpVecEnv(4096, seed=4, infos=False)
+    model = PPO("MlpPolicy", env, n_steps=16, batch_size=4096, n_epochs=4, seed=0, use_graphs=True,
+                fused_update=False, collect="lockstep")
+    seen, graphs = _graph_vs_eager_checker(model)
+    probe = torch.randn(4096, env.sim.obs_dim, device=model.device)
+    for _ in range(4):
+        model.learn(model.num_timesteps + 16 * 4096)
+        with torch.no_grad():   # eager GEMMs on the default stream, as an evaluation callback would issue
+            for _ in range(3):
+                model.policy.value(probe)
+                model.policy.act(probe)
+    assert sorted(seen) == [2, 3, 4] and all(seen.values()), seen
+    assert len(set(graphs)) == 1, "the graph was recaptured"
+    env.close()

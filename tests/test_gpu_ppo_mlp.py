@@ -140,15 +140,20 @@ def test_fused_step_equals_torch_clip_and_adam():
     assert torch.allclose(acc_a, acc_t, rtol=1e-4, atol=1e-6)
 
 
-def test_fused_graph_is_kept_and_equals_eager():
-    """PPO with the fused step on one GPU replays one graph per epoch, captured
-    in the first update and kept for every later one; three iterations leave
-    exactly (bit for bit: no atomics) the parameters, Adam state and losses of
-    the same learner stepping every minibatch eagerly, and stay finite."""
+@pytest.mark.parametrize("max_mb", [1024, 3])
+def test_fused_graph_is_kept_and_equals_eager(max_mb):
+    """PPO with the fused step on one GPU replays one graph per epoch (or, with
+    max_graph_minibatches 3, a graph of 2 of the epoch's 8 minibatches four
+    times), captured in the first update and kept for every later one; three
+    iterations leave exactly (bit for bit: no atomics) the parameters, Adam
+    state and losses of the same learner stepping every minibatch eagerly, and
+    stay finite."""
     out = []
     for graphs in (True, False):
         env = SalpVecEnv(32768, seed=0, infos=False)
-        model = PPO("MlpPolicy", env, n_steps=8, batch_size=32768, n_epochs=2, seed=0, use_graphs=graphs)
+        model = PPO("MlpPolicy", env, n_steps=8, batch_size=32768, n_epochs=2, seed=0, use_graphs=graphs,
+                    max_graph_minibatches=max_mb)
+        assert model._graph_chunk(8) == (8 if max_mb >= 8 else 2)
         assert model.fused_update and model.use_graphs == graphs
         ids = []
         for _ in range(3):

@@ -34,6 +34,10 @@ def main():
                  torch.zeros(1, dtype=torch.int64, device="cuda"))
         out = {"n_envs": n, "k": k}
         for rep in range(2):
+            # salp_collect acts first on last_obs (in/out): the env's reset
+            # observation, as PPO hands it over (the other legs moved the state)
+            extra[1].copy_(env.reset())
+            extra[0].fill_(1.0)
             out[f"collect_{rep}"] = n * k / timed(lambda: env.collect(w, k, bufs, *extra, diverged_obs_abs=1e3,
                                                                        diverged_reward_abs=1e4)) / 1e6
             sd = torch.zeros(n, dtype=torch.int64, device="cuda")

@@ -17,7 +17,21 @@ from grasp_lab_salp_amd.salp_robot_env import SalpRobotEnv  # noqa: E402
 from grasp_lab_salp_amd.vec_env import SalpVecEnv  # noqa: E402
 
 
-def vec_rate(n, steps, infos):
+def _read_done(dones, infos):
+    """What SB3's collect_rollouts / Monitor buffer read: the envs that finished."""
+    for i in np.nonzero(dones)[0]:
+        d = infos[i]
+        d["episode"], d["terminal_observation"], d.get("TimeLimit.truncated")
+
+
+def _scan(dones, infos):
+    """src/tensorboard_callback.py:72: `for idx, info in enumerate(infos): if 'episode' in info`."""
+    for _idx, info in enumerate(infos):
+        if "episode" in info:
+            info["episode"]["r"]
+
+
+def vec_rate(n, steps, infos, consume=None):
     env = SalpVecEnv(n, seed=0, infos=infos)
     env.reset()
     rng = np.random.default_rng(0)
@@ -28,7 +42,9 @@ def vec_rate(n, steps, infos):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for a in acts[2:]:
-        env.step(a)
+        _, _, dones, inf = env.step(a)
+        if consume is not None:
+            consume(dones, inf)
     el = time.perf_counter() - t0
     env.close()
     return n * steps / el
@@ -58,11 +74,15 @@ def main():
     out = {"n_envs": n,
            "vec_env_infos_off": vec_rate(n, 10, False),
            "vec_env_infos_on": vec_rate(n, 10, True),
+           "vec_env_infos_on_sb3_done_reads": vec_rate(n, 10, True, _read_done),
+           "vec_env_infos_on_full_scan": vec_rate(n, 4, True, _scan),
            "gym_env_single": gym_rate(200),
            "unit": "env-steps/s",
            "note": "host clock around whole steps: NumPy actions uploaded, salp_step, obs/reward/flags (and info "
-                   "dicts of the envs that finished) downloaded; the device-resident rate is bench.py's "
-                   "step_given_actions_env_steps_per_sec"}
+                   "dicts of the envs that finished) downloaded; infos are built on access (vec_env.StepInfos): "
+                   "_sb3_done_reads reads the finished envs' episode / terminal_observation / TimeLimit entries "
+                   "as SB3 does, _full_scan visits every env's dict as src/tensorboard_callback.py:72 does; the "
+                   "device-resident rate is bench.py's step_given_actions_env_steps_per_sec"}
     print(json.dumps(out), flush=True)
 
 

@@ -6,7 +6,10 @@ Reads gpurun_out/pmc_<TAG>_<pass>/run_counter_collection.csv and writes
 profiles/<TAG>_pmc_summary.json: per-dispatch means of every counter, the HBM
 bytes per dispatch (FETCH_SIZE and WRITE_SIZE are KiB; FETCH_SIZE doubled, the
 gfx950 correction of MI355X_MICROARCH.md §HBM) and fp64 VALU counts.  bench.py
-reports `roofline.traffic` from the summary whose config matches its own.
+reports `roofline.traffic` from the summary whose config matches its own and
+whose `kernel_sha16` (the counted kernel's machine-code fingerprint,
+grasp_lab_salp_amd/_codeobj.py) equals the one of the library it ran: run this
+on the tree whose libsalp.so the passes profiled.
 """
 import argparse
 import collections
@@ -14,14 +17,19 @@ import csv
 import glob
 import json
 import os
+import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from grasp_lab_salp_amd import _codeobj  # noqa: E402
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
     ap.add_argument("--kernel", default="k_rollout")
+    ap.add_argument("--symbol", default=_codeobj.ROLLOUT_KERNEL,
+                    help="mangled-name fragment of the counted instance (fingerprint)")
     ap.add_argument("--n-envs", type=int, default=65536)
     ap.add_argument("--tick-budget", type=int, default=8192)
     ap.add_argument("--chunk", type=int, default=128)
@@ -43,6 +51,8 @@ def main():
            "config": {"n_envs": a.n_envs, "tick_budget": a.tick_budget, "chunk": a.chunk},
            "command": "tools/gpu_pmc.sh: rocprofv3 --pmc <group> --kernel-trace -- python3 bench.py "
                       "--steps 2 --warmup 1 --no-cpu-baseline --no-lockstep --no-parity-check --no-ppo, one pass per group",
+           "kernel_symbol": a.symbol,
+           "kernel_sha16": _codeobj.kernel_sha(os.path.join(ROOT, "grasp_lab_salp_amd", "libsalp.so"), a.symbol),
            "per_dispatch": per, "derived": {}}
     d = out["derived"]
     if g("FETCH_SIZE") is not None:
