@@ -6,7 +6,7 @@ drift apart silently.
 """
 import ctypes
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 MAX_OBSTACLES = 4
 OBS_DIM_MAX = 6 + 2 * MAX_OBSTACLES
 

@@ -128,6 +128,7 @@ SIGNATURES = {
     "salp_lstm_step_forward": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
     "salp_lstm_step_backward": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32] + [_V] * 11),
     "salp_set_lockstep_order": (ctypes.c_int, [_H, ctypes.c_int]),
+    "salp_set_rollout_kernel": (ctypes.c_int, [_H, ctypes.c_int]),
     "salp_robot_reset": (ctypes.c_int, [_H, _V, _V]),
     "salp_nozzle_set_angles": (ctypes.c_int, [_H, _V, _V]),
     "salp_nozzle_solve": (ctypes.c_int, [_H, _V, ctypes.c_int, _V]),

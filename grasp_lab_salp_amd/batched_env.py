@@ -185,6 +185,14 @@ class BatchedSalpEnv:
         in every mode."""
         self._check(_lib.load().salp_set_lockstep_order(self._h, int(mode)))
 
+    def set_rollout_kernel(self, mode):
+        """Kernel of :meth:`rollout`, :meth:`collect` and chained
+        :meth:`step_random` (salp_set_rollout_kernel): 1 = two waves per env
+        (k_rollout_pair), 0 = one env per lane (k_rollout), -1 = the pair
+        kernel up to 128 envs per compute unit (default).  Results are
+        identical in every mode."""
+        self._check(_lib.load().salp_set_rollout_kernel(self._h, int(mode)))
+
     def rollout(self, tick_budget, buffers=None, steps_done=None, max_steps=0, chunk=128):
         """Chained random-action rollout: each env runs ``tick_budget`` physics
         ticks, completing as many env-steps as fit (auto-reset).  ``buffers`` is

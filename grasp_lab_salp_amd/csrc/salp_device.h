@@ -259,6 +259,8 @@ struct Geo {
  * A1 = area[1] = area[2]; compute_drag_coefficient_jit (src/geometry.py:
  * 104-123): the clipped interpolation ratio nr of the coefficient ranges. */
 struct Shape { double A0, A1, nr; };
+/* compute_jet_moment_arm_jit (src/geometry.py:126-130), x component */
+SD double jet_arm(const Params& P, double L) { return P.mid_x + -L / 2.0; }
 SD Shape shape_of(const Params& P, const Core& c, double L, double W, bool f) {
     Shape s;
     double pi = sel(f, PI);
@@ -275,10 +277,14 @@ SD double tcd_x(double nr) { return 2.5 - nr * (2.5 - 1.5); }
 SD double tcd_y(double nr) { return 1.5 - nr * (1.5 - 2.5); }
 SD double rcd_x(double nr) { return 0.3 - nr * (0.3 - 0.1); }
 SD double rcd_y(double nr) { return 0.2 - nr * (0.2 - 0.5); }
-SD Geo make_geo_shape(const Params& P, const Core& c, double L, double W, double wm, bool f) {
-    Geo g;
-    /* get_mass (src/robot.py:1061-1066); wm = water mass */
-    g.m = r32(r32(sel(f, P.dry_mass) + wm, f) + sel(f, P.nozzle_mass), f);
+/* get_mass (src/robot.py:1061-1066); wm = water mass */
+SD double geo_mass(const Params& P, double wm, bool f) {
+    return r32(r32(sel(f, P.dry_mass) + wm, f) + sel(f, P.nozzle_mass), f);
+}
+/* Everything of make_geo_shape but the mass: drag coefficients, body cubes,
+ * inertia and jet moment arm (the shape side, which k_rollout_pair's B wave
+ * computes while the A wave does the mass side). */
+SD void geo_shape(const Params& P, const Core& c, double L, double W, bool f, Geo& g) {
     const Shape sh = shape_of(P, c, L, W, f);
     const double A0 = sh.A0, A1 = sh.A1, nr = sh.nr;
     /* compute_drag_force_jit / compute_drag_torque_jit coefficients
@@ -303,7 +309,12 @@ SD Geo make_geo_shape(const Params& P, const Core& c, double L, double W, double
     g.I1 = BUOY_MASS * c.lh2 + P.net_tube_mass * t8 + r32(p1 * sy, f) + r32(kw * sy, f) +
            P.nozzle_mass * n25;
     /* compute_jet_moment_arm_jit (src/geometry.py:126-130) */
-    g.rx = P.mid_x + -L / 2.0;
+    g.rx = jet_arm(P, L);
+}
+SD Geo make_geo_shape(const Params& P, const Core& c, double L, double W, double wm, bool f) {
+    Geo g;
+    g.m = geo_mass(P, wm, f);
+    geo_shape(P, c, L, W, f, g);
     return g;
 }
 /* get_mass_rate (src/robot.py:651-654) and compute_jet_velocity_jit speed
@@ -348,8 +359,9 @@ enum { C32_V, C32_WM, C32_COM, C32_M, C32_I0, C32_I1, C32_KC0, C32_KC1, C32_RA0,
        C32_DIMY, C32_N };
 constexpr int LANES = 256;   /* workgroup size of every ticking kernel (LDS stride) */
 struct Cache32 {
-    double* p;               /* this lane's column of a [C32_N][LANES] LDS array */
-    SD_MEMBER double& operator[](int k) const { return p[k * LANES]; }
+    double* p;               /* this lane's column of a [C32_N][stride] LDS array */
+    int stride = LANES;      /* slots of the array: LANES, or k_rollout_pair's envs per workgroup */
+    SD_MEMBER double& operator[](int k) const { return p[k * stride]; }
 };
 SD void fill_cache32(const Params& P, double contraction, Cache32 c32) {
     const double L = (double)((float)P.L0 - (float)contraction);
@@ -1429,7 +1441,8 @@ SD void store_cold(const ColdRegs<RAND>& C, double* S, const Params& P, int64_t 
 constexpr int SPILL_N = 63;
 struct SpillSlot {
     double* p;
-    SD_MEMBER double& operator[](int k) const { return p[k * LANES]; }
+    int stride = LANES;
+    SD_MEMBER double& operator[](int k) const { return p[k * stride]; }
 };
 template <bool RAND>
 SD void spill(const Hot& h, SpillSlot s) {

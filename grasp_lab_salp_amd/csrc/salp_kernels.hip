@@ -13,6 +13,7 @@
 #include <string>
 
 #include "salp_device.h"
+#include "salp_pair.h"
 
 using salp::Hot;
 using salp::Params;
@@ -749,6 +750,370 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
 }
 #endif
 
+// ----------------------------------------------------------------------
+// k_rollout_pair: the chained rollout with every env on TWO waves
+// (salp_pair.h).  A workgroup is 4 waves = 2 groups of 64 envs; wave 2g is
+// group g's A wave, wave 2g + 1 its B wave, and lane l of both holds the same
+// env.  128 env slots per workgroup, re-seated at every chunk boundary like
+// k_rollout (unsteady envs first).  Env-step boundaries run on the A waves
+// with the whole state assembled in the slot; inside a chunk the two waves of
+// a group meet once per tick through LDS (two packet buffers per direction,
+// a release/acquire counter per wave; no workgroup barrier), and the A wave
+// decides each tick's kind (full / steady / settled / end of chunk) exactly as
+// k_rollout's loops do and sends it with its packet.  Same per-env results as
+// k_rollout.
+constexpr int kPairEnvs = 128;
+constexpr int kXchAB = 5;    // A -> B: v x (M_a v) (3), jet torque y, z
+constexpr int kXchBA = 12;   // B -> A: w (3), alpha y, z, sin/cos roll, pitch (4), yaw, drag-force coefficients (2)
+constexpr int kXchBase = 4 * kXchAB * 64;                           // first double of the B -> A packets
+constexpr int kXchDoubles = kXchBase + 4 * kXchBA * 64;
+static_assert(kXchDoubles <= salp::SPILL_N * kPairEnvs, "the packets live in the spill slots' LDS");
+// A wave gives up on its partner after this many polls (s_sleep 1 = 64 cycles
+// each, ~0.1 s): the kernel always ends (a broken pair gives garbage, which the
+// parity tests see, instead of a hung GPU); counted in g_pair_timeouts.
+constexpr int kPairSpin = 1 << 21;
+__device__ unsigned int g_pair_timeouts;
+
+// SALP_PAIR_PROF=1 (experiment builds only, tools/build_variant.py): s_memtime
+// cycles per wave and phase, summed over the launch's waves into
+// g_pair_prof[role][phase] (read back by salp_debug_pair_prof).
+#ifndef SALP_PAIR_PROF
+#define SALP_PAIR_PROF 0
+#endif
+enum { PP_BOUNDARY, PP_TICK, PP_PUBLISH, PP_WAIT, PP_READ, PP_WORLD, PP_N };
+__device__ unsigned long long g_pair_prof[2][PP_N];
+struct PairProf {
+    unsigned long long acc[PP_N] = {};
+    unsigned long long t = 0;
+    __device__ __forceinline__ void start() {
+        if (SALP_PAIR_PROF) t = __builtin_amdgcn_s_memtime();
+    }
+    __device__ __forceinline__ void lap(int phase) {
+        if (SALP_PAIR_PROF) {
+            const unsigned long long now = __builtin_amdgcn_s_memtime();
+            acc[phase] += now - t;
+            t = now;
+        }
+    }
+    __device__ __forceinline__ void flush(int role) {
+        if (SALP_PAIR_PROF && (threadIdx.x & 63) == 0)
+            for (int k = 0; k < PP_N; ++k) atomicAdd(&g_pair_prof[role][k], acc[k]);
+    }
+};
+
+struct PairShared {
+    double cache32[salp::C32_N * kPairEnvs];
+    double big[salp::SPILL_N * kPairEnvs];   // spill slots between chunks | tick packets inside a chunk
+    int64_t steps[kPairEnvs];
+    int16_t slot[2][kPairEnvs];
+    uint64_t mask[2][2], amask[2][2];
+    int cnt[2][2];                            // [group][role]: packets published
+    int mode[2][2];                           // [group][buffer]: the tick kind wave A sent
+    uint8_t flags[kPairEnvs];
+};
+
+__device__ __forceinline__ bool pair_wait(int* flag, int target) {
+    for (int it = 0; it < kPairSpin; ++it) {
+        if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_pair_timeouts, 1u);
+    return false;
+}
+__device__ __forceinline__ void pair_publish(int* flag, int value) {
+    __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Position of the k-th set bit of the 128-bit mask m[0..1] (k < popcount).
+__device__ __forceinline__ int nth_set_seat(const uint64_t* m, int k) {
+    const int c0 = __popcll(m[0]);
+    uint64_t w = k < c0 ? m[0] : m[1];
+    int base = k < c0 ? 0 : 64;
+    if (k >= c0) k -= c0;
+    int pos = 0;
+#pragma unroll
+    for (int half = 32; half > 0; half >>= 1) {
+        const uint64_t lo = w & ((1ull << half) - 1ull);
+        const int c = __popcll(lo);
+        if (k >= c) {
+            k -= c;
+            w >>= half;
+            pos += half;
+        } else {
+            w = lo;
+        }
+    }
+    return base + pos;
+}
+
+// The slot state's unsteady flag (k_rollout's `unsteady`), read from the slot.
+__device__ __forceinline__ bool slot_unsteady(salp::SpillSlot sl, const Params& P, bool active) {
+    double mx, b1, b2;
+    salp::cycle_bounds_of(sl[salp::SP_REFILL], sl[salp::SP_TURN], sl[salp::SP_JET], sl[salp::SP_COAST], &mx, &b1,
+                          &b2);
+    const double ct = sl[salp::SP_CT];
+    const bool g32 = (((int)sl[salp::SP_FLAGS]) & 4) != 0;
+    return active && ct < b2 && !salp::pair_next_steady(ct, sl[salp::SP_L], sl[salp::SP_WID], g32, b1, mx, P);
+}
+
+// Re-seat after the boundary: the seat's new slot and its bookkeeping (both
+// waves of a group compute the same assignment).
+__device__ __forceinline__ void pair_reseat(PairShared& sh, int b, int seat, int& s, int64_t& steps, bool& pending,
+                                            bool& active, bool& all_done) {
+    uint64_t m[2] = {sh.mask[b][0], sh.mask[b][1]};
+    const int n_uns = __popcll(m[0]) + __popcll(m[1]);
+    all_done = (sh.amask[b][0] | sh.amask[b][1]) == 0;
+    int from;
+    if (seat < n_uns) {
+        from = nth_set_seat(m, seat);
+    } else {
+        m[0] = ~m[0];
+        m[1] = ~m[1];
+        from = nth_set_seat(m, seat - n_uns);
+    }
+    s = sh.slot[b][from];
+    const int fl = sh.flags[s];
+    pending = (fl & 1) != 0;
+    active = (fl & 2) != 0;
+    steps = sh.steps[s];
+}
+
+template <bool POL>
+__device__ __forceinline__ void pair_wave_a(PairShared& sh, const RolloutArgs& A, int grp, int lane) {
+    const Params& P = A.P;
+    const int seat = grp * 64 + lane;
+    const int64_t base = (int64_t)blockIdx.x * kPairEnvs;
+    int s = seat;
+    int64_t i = base + s;
+    bool pending = false, active = false;
+    int64_t steps = 0;
+    {   // load this seat's env into its slot (the whole state)
+        double* const S = A.S;
+        Hot h{};
+        if (i < P.n) {
+            pending = !A.fresh && SF(SALP_F_PENDING) != 0.0;
+            steps = A.B.steps_done ? A.B.steps_done[i] : 0;
+            active = !(A.max_steps > 0 && steps >= A.max_steps);
+            salp::load_hot<false>(h, S, P, i);
+            salp::resume_cycle(h, S, P, i);
+            salp::fill_cache32(P, h.c, salp::Cache32{sh.cache32 + s, kPairEnvs});
+        }
+        salp::spill<false>(h, salp::SpillSlot{sh.big + s, kPairEnvs});
+        if (lane < 2) sh.cnt[grp][lane] = 0;
+    }
+    __syncthreads();   // #0
+    int pub = 0, rcv = 0;
+    bool all_done = false;
+    PairProf prof;
+    prof.start();
+    for (int64_t c = 0;; ++c) {
+        const bool last = c == A.n_chunks || all_done;
+        const salp::SpillSlot sl{sh.big + s, kPairEnvs};
+        bool need;
+        {
+            double mx, b1, b2;
+            salp::cycle_bounds_of(sl[salp::SP_REFILL], sl[salp::SP_TURN], sl[salp::SP_JET], sl[salp::SP_COAST], &mx,
+                                  &b1, &b2);
+            need = active && (!pending || !(sl[salp::SP_CT] < b2));
+        }
+        if (need) {
+            const RolloutArgs a = fresh_args();
+            const uint64_t env_id = (uint64_t)(a.P.env_offset + i);
+            salp::ColdRegs<false> C;
+            salp::load_cold<false>(C, a.S, a.P, i);
+            Hot hb;
+            salp::unspill<false>(hb, sl, a.P, env_id);
+            rollout_boundary<false, POL>(hb, &C, a.P, i, env_id, pending, active, steps, a.max_steps, a.B,
+                                         a.reward_sum, a.R, salp::Cache32{sh.cache32 + s, kPairEnvs});
+            salp::store_cold<false>(C, a.S, a.P, i);
+            salp::spill<false>(hb, sl);
+        }
+        if (last) {
+            const RolloutArgs a = fresh_args();
+            Hot h;
+            salp::unspill<false>(h, sl, a.P, (uint64_t)(a.P.env_offset + i));
+            if (i < a.P.n) {
+                salp::store_hot<false>(h, a.S, a.P, i);
+                if (a.B.steps_done) a.B.steps_done[i] = steps;
+            }
+            prof.lap(PP_BOUNDARY);
+            prof.flush(0);
+            return;
+        }
+        const bool uns = slot_unsteady(sl, P, active);
+        const int b = (int)(c & 1);
+        sh.steps[s] = steps;
+        sh.flags[s] = (uint8_t)((pending ? 1 : 0) | (active ? 2 : 0));
+        sh.slot[b][seat] = (int16_t)s;
+        const uint64_t ballot = __ballot(uns), aballot = __ballot(active);
+        if (lane == 0) {
+            sh.mask[b][grp] = ballot;
+            sh.amask[b][grp] = aballot;
+        }
+        __syncthreads();   // #1
+        pair_reseat(sh, b, seat, s, steps, pending, active, all_done);
+        i = base + s;
+        if (all_done) continue;
+        const salp::SpillSlot ns{sh.big + s, kPairEnvs};
+        const salp::Cache32 c32{sh.cache32 + s, kPairEnvs};
+        salp::HotA h;
+        salp::unspill_a(h, ns);
+        if (!active) h.b2 = -INFINITY;
+        __syncthreads();   // #2: slots read; the packets may overwrite them now
+        {
+            const Params PV = salp::pin_params(P);
+            const int chunk = A.chunk, q8 = A.steady_q8;
+            double* const ab = sh.big + grp * 2 * kXchAB * 64 + lane;
+            double* const ba = sh.big + kXchBase + grp * 2 * kXchBA * 64 + lane;
+            int k = 0, j = 0, ks = 0, stage = 0;
+            const auto decide = [&]() -> int {
+                if (stage == 0) {
+                    if (k < chunk && !__all(!(h.ct < h.b2) ||
+                                            salp::pair_next_steady(h.ct, h.L, h.W, h.g32, h.b1, h.mx, PV))) {
+                        ++k;
+                        return salp::PM_FULL;
+                    }
+                    ks = (int32_t)(((int64_t)(chunk - k) * q8) >> 8);
+                    stage = 1;
+                }
+                if (j >= ks) return salp::PM_END;
+                ++j;
+                return stage == 1 ? salp::PM_STEADY : salp::PM_SETTLED;
+            };
+            const auto publish = [&](int mode) {
+                double X[3], jt[2];
+                salp::a_prepare(h, PV, X, jt);
+                double* const o = ab + (pub & 1) * kXchAB * 64;
+                o[0 * 64] = X[0]; o[1 * 64] = X[1]; o[2 * 64] = X[2]; o[3 * 64] = jt[0]; o[4 * 64] = jt[1];
+                if (lane == 0) sh.mode[grp][pub & 1] = mode;
+                pair_publish(&sh.cnt[grp][0], ++pub);
+            };
+            bool ok = true;
+            const auto recv = [&]() {
+                prof.lap(PP_PUBLISH);
+                ok = pair_wait(&sh.cnt[grp][1], rcv + 1) && ok;
+                prof.lap(PP_WAIT);
+                const double* const q = ba + (rcv & 1) * kXchBA * 64;
+                h.w0 = q[0 * 64]; h.w1 = q[1 * 64]; h.w2 = q[2 * 64]; h.al1 = q[3 * 64]; h.al2 = q[4 * 64];
+                h.sp = q[5 * 64]; h.cp = q[6 * 64]; h.st = q[7 * 64]; h.cth = q[8 * 64]; h.e2 = q[9 * 64];
+                h.kc0 = q[10 * 64]; h.kc1 = q[11 * 64];
+                ++rcv;
+                prof.lap(PP_READ);
+            };
+            prof.lap(PP_BOUNDARY);
+            int mode = decide();
+            publish(mode);
+            recv();
+            while (mode != salp::PM_END && ok) {
+                const bool ticks = h.ct < h.b2;
+                if (mode == salp::PM_FULL) {
+                    if (ticks) salp::tick_a<salp::PM_FULL>(h, PV, c32);
+                } else if (mode == salp::PM_STEADY) {
+                    bool settled = true;
+                    if (ticks) settled = salp::tick_a<salp::PM_STEADY>(h, PV, c32);
+                    if (__all(settled)) stage = 2;
+                } else {
+                    if (ticks) salp::tick_a<salp::PM_SETTLED>(h, PV, c32);
+                }
+                mode = decide();
+                prof.lap(PP_TICK);
+                publish(mode);
+                recv();
+                if (ticks) salp::a_world(h, PV);
+                prof.lap(PP_WORLD);
+            }
+        }
+        __syncthreads();   // #3: packets done
+        salp::spill_a(h, ns, P);
+        __syncthreads();   // #4: slots whole again
+    }
+}
+
+__device__ __forceinline__ void pair_wave_b(PairShared& sh, const RolloutArgs& A, int grp, int lane) {
+    const Params& P = A.P;
+    const int seat = grp * 64 + lane;
+    int s = seat;
+    bool pending = false, active = false;
+    int64_t steps = 0;
+    {   // the A wave loaded the slots; the bookkeeping comes with the re-seat
+        const int64_t i = (int64_t)blockIdx.x * kPairEnvs + s;
+        if (i < P.n) {
+            steps = A.B.steps_done ? A.B.steps_done[i] : 0;
+            active = !(A.max_steps > 0 && steps >= A.max_steps);
+        }
+    }
+    __syncthreads();   // #0
+    int pub = 0, rcv = 0;
+    bool all_done = false;
+    PairProf prof;
+    prof.start();
+    for (int64_t c = 0;; ++c) {
+        const bool last = c == A.n_chunks || all_done;
+        if (last) {
+            prof.lap(PP_BOUNDARY);
+            prof.flush(1);
+            return;
+        }
+        const int b = (int)(c & 1);
+        __syncthreads();   // #1
+        pair_reseat(sh, b, seat, s, steps, pending, active, all_done);
+        if (all_done) continue;
+        const salp::SpillSlot ns{sh.big + s, kPairEnvs};
+        const salp::Cache32 c32{sh.cache32 + s, kPairEnvs};
+        salp::HotB h;
+        salp::unspill_b(h, ns, P);
+        if (!active) h.b2 = -INFINITY;
+        __syncthreads();   // #2
+        {
+            const Params PV = salp::pin_params(P);
+            double* const ab = sh.big + grp * 2 * kXchAB * 64 + lane;
+            double* const ba = sh.big + kXchBase + grp * 2 * kXchBA * 64 + lane;
+            const auto publish = [&]() {
+                double* const o = ba + (pub & 1) * kXchBA * 64;
+                o[0 * 64] = h.w0; o[1 * 64] = h.w1; o[2 * 64] = h.w2; o[3 * 64] = h.al1; o[4 * 64] = h.al2;
+                o[5 * 64] = h.sp; o[6 * 64] = h.cp; o[7 * 64] = h.st; o[8 * 64] = h.cth; o[9 * 64] = h.e2;
+                o[10 * 64] = h.kc0; o[11 * 64] = h.kc1;
+                pair_publish(&sh.cnt[grp][1], ++pub);
+            };
+            // a bound on the ticks of one chunk (A ends it earlier)
+            const int64_t cap = 4 + (int64_t)A.chunk + (((int64_t)A.chunk * A.steady_q8) >> 8);
+            prof.lap(PP_BOUNDARY);
+            publish();
+            prof.lap(PP_PUBLISH);
+            for (int64_t it = 0; it < cap; ++it) {
+                const bool ok = pair_wait(&sh.cnt[grp][0], rcv + 1);
+                prof.lap(PP_WAIT);
+                const double* const q = ab + (rcv & 1) * kXchAB * 64;
+                h.X0 = q[0 * 64]; h.X1 = q[1 * 64]; h.X2 = q[2 * 64]; h.jt1 = q[3 * 64]; h.jt2 = q[4 * 64];
+                const int mode = __builtin_amdgcn_readfirstlane(sh.mode[grp][rcv & 1]);
+                ++rcv;
+                prof.lap(PP_READ);
+                if (mode == salp::PM_END || !ok) break;
+                if (h.ct < h.b2) {
+                    if (mode == salp::PM_FULL) salp::tick_b<salp::PM_FULL>(h, PV, c32);
+                    else if (mode == salp::PM_STEADY) salp::tick_b<salp::PM_STEADY>(h, PV, c32);
+                    else salp::tick_b<salp::PM_SETTLED>(h, PV, c32);
+                }
+                prof.lap(PP_TICK);
+                publish();
+                prof.lap(PP_PUBLISH);
+            }
+        }
+        __syncthreads();   // #3
+        salp::spill_b(h, ns);
+        __syncthreads();   // #4
+    }
+}
+
+template <bool POL>
+__global__ __launch_bounds__(kBlock) void k_rollout_pair(RolloutArgs A) {
+    __shared__ PairShared sh;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = (int)(threadIdx.x & 63);
+    if (wave & 1) pair_wave_b(sh, A, wave >> 1, lane);
+    else pair_wave_a<POL>(sh, A, wave >> 1, lane);
+}
+
 // The ABI's field-major state (state[f * n + i]) <-> the handle's layout
 // (field-major rows + env-major cold block, salp_device.h "state layout").
 // One env per lane; the field-major side is coalesced per field.
@@ -893,6 +1258,8 @@ struct SalpEnv {
     void* sort_temp = nullptr;
     size_t sort_temp_bytes = 0;
     int64_t* step_counts = nullptr;   // per-env env-step counter of a chained salp_step_random
+    int rollout_kernel = -1;          // salp_set_rollout_kernel: -1 auto, 0 k_rollout, 1 k_rollout_pair
+    int cu_count = 256;               // compute units of the device (the auto choice)
 };
 
 namespace {
@@ -928,6 +1295,39 @@ int32_t rollout_steady_q8() {
 
 // Any randomisation switch on: launch the RAND instantiation of the kernels.
 bool randomized(const Params& d) { return d.rand_dyn || d.rand_dist || d.rand_act || d.rand_obs || d.latency; }
+
+// The chained kernels (salp_rollout, salp_collect, chained salp_step_random):
+// k_rollout_pair (two waves per env, salp_pair.h) or k_rollout (one lane per
+// env).  Auto: the pair kernel while one env per lane would leave SIMDs
+// without a wave (n <= 64 lanes x 4 SIMDs x CUs / 2, e.g. config 5's 32 768
+// envs); SALP_ROLLOUT_KERNEL=0/1 overrides the auto choice (A/B runs).
+// The pair kernel has no randomised instance.
+bool use_pair(const SalpEnv* h) {
+    if (randomized(h->dp)) return false;
+    if (h->rollout_kernel == 0 || h->rollout_kernel == 1) return h->rollout_kernel == 1;
+    static const int forced = [] {
+        const char* e = std::getenv("SALP_ROLLOUT_KERNEL");
+        return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
+    }();
+    if (forced >= 0) return forced == 1;
+    return h->n <= (int64_t)h->cu_count * 128;
+}
+unsigned pair_blocks_for(int64_t n) { return (unsigned)((n + kPairEnvs - 1) / kPairEnvs); }
+
+// One chained launch on the kernel use_pair chooses.
+int launch_chained(SalpEnv* h, const RolloutArgs& args, bool pol, hipStream_t st, const char* what) {
+    if (use_pair(h)) {
+        hipLaunchKernelGGL(pol ? k_rollout_pair<true> : k_rollout_pair<false>, dim3(pair_blocks_for(h->n)),
+                           dim3(kBlock), 0, st, args);
+    } else if (pol) {
+        hipLaunchKernelGGL((randomized(h->dp) ? k_rollout<true, true> : k_rollout<false, true>),
+                           dim3(blocks_for(h->n)), dim3(kBlock), 0, st, args);
+    } else {
+        hipLaunchKernelGGL((randomized(h->dp) ? k_rollout<true, false> : k_rollout<false, false>),
+                           dim3(blocks_for(h->n)), dim3(kBlock), 0, st, args);
+    }
+    return launched(h, what);
+}
 
 // Launch-invariant constants; the same IEEE expressions as the oracle.
 Params derive(const SalpParams& p, int64_t n, uint64_t seed, int64_t offset) {
@@ -1035,6 +1435,11 @@ int salp_create(const SalpParams* p, int64_t n_envs, uint64_t seed, int64_t env_
     h->dp = derive(*p, n_envs, seed, env_id_offset);
     int rc = check_hip(nullptr, hipSetDevice(device), "hipSetDevice");
     if (rc) { delete h; return rc; }
+    {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+            h->cu_count = cus;
+    }
     rc = check_hip(nullptr, hipMalloc(&h->state, sizeof(double) * (size_t)salp::layout_doubles(n_envs)),
                    "hipMalloc(state)");
     if (rc) { delete h; return SALP_ENOMEM; }
@@ -1174,9 +1579,7 @@ int salp_step_random(SalpEnv* h, int32_t n_steps, double* reward_sum_out, void* 
         // bound: n_steps cycles of the longest legitimate length (the lock-step guard)
         const int64_t n_chunks = ((int64_t)n_steps * kMaxTicksPerCycle + chunk - 1) / chunk;
         RolloutArgs args{h->state, h->dp, n_chunks, chunk, rollout_steady_q8(), n_steps, b, reward_sum_out, 1, 0};
-        hipLaunchKernelGGL((randomized(h->dp) ? k_rollout<true, false> : k_rollout<false, false>), dim3(blocks_for(h->n)),
-                           dim3(kBlock), 0, st, args);
-        return launched(h, "k_rollout(step_random)");
+        return launch_chained(h, args, false, st, "k_rollout(step_random)");
     }
     const int32_t* order = lockstep_order(h, nullptr, n_steps, stream, &rc);
     if (rc) return rc;
@@ -1194,9 +1597,7 @@ int salp_rollout(SalpEnv* h, int64_t tick_budget, const SalpRolloutBuffers* buf,
     int32_t chunk = b.chunk > 0 ? b.chunk : 128;
     int64_t n_chunks = (tick_budget + chunk - 1) / chunk;
     RolloutArgs args{h->state, h->dp, n_chunks, chunk, rollout_steady_q8(), b.max_steps, b, nullptr, 0, 0};
-    hipLaunchKernelGGL((randomized(h->dp) ? k_rollout<true, false> : k_rollout<false, false>), dim3(blocks_for(h->n)),
-                       dim3(kBlock), 0, (hipStream_t)stream, args);
-    return launched(h, "k_rollout");
+    return launch_chained(h, args, false, (hipStream_t)stream, "k_rollout");
 }
 
 int salp_collect(SalpEnv* h, const SalpPolicyRollout* r, void* stream) {
@@ -1225,9 +1626,7 @@ int salp_collect(SalpEnv* h, const SalpPolicyRollout* r, void* stream) {
     }();
     const int64_t n_chunks = (r->n_steps * kMaxTicksPerCycle + chunk - 1) / chunk;
     RolloutArgs args{h->state, h->dp, n_chunks, chunk, rollout_steady_q8(), r->n_steps, b, nullptr, 1, 0, *r};
-    hipLaunchKernelGGL((randomized(h->dp) ? k_rollout<true, true> : k_rollout<false, true>), dim3(blocks_for(h->n)),
-                       dim3(kBlock), 0, st, args);
-    return launched(h, "k_rollout(collect)");
+    return launch_chained(h, args, true, st, "k_rollout(collect)");
 }
 
 int salp_robot_reset(SalpEnv* h, const uint8_t* mask, void* stream) {
@@ -1276,6 +1675,22 @@ int salp_set_lockstep_order(SalpEnv* h, int mode) {
     if (!h) return fail(nullptr, SALP_EINVAL, "salp_set_lockstep_order: null handle");
     if (mode < -1 || mode > 1) return fail(h, SALP_EINVAL, "salp_set_lockstep_order: mode must be -1, 0 or 1");
     h->order_mode = mode;
+    return SALP_OK;
+}
+
+#if SALP_PAIR_PROF
+// experiment builds only (not in include/salp.h): read and clear g_pair_prof
+int salp_debug_pair_prof(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pair_prof), sizeof(g_pair_prof)) != hipSuccess) return -1;
+    static const unsigned long long zero[2][PP_N] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_pair_prof), zero, sizeof zero) == hipSuccess ? 0 : -1;
+}
+#endif
+
+int salp_set_rollout_kernel(SalpEnv* h, int mode) {
+    if (!h) return fail(nullptr, SALP_EINVAL, "salp_set_rollout_kernel: null handle");
+    if (mode < -1 || mode > 1) return fail(h, SALP_EINVAL, "salp_set_rollout_kernel: mode must be -1, 0 or 1");
+    h->rollout_kernel = mode;
     return SALP_OK;
 }
 

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define SALP_ABI_VERSION 8
+#define SALP_ABI_VERSION 9
 
 #define SALP_MAX_OBSTACLES 4
 #define SALP_OBS_DIM_MAX (6 + 2 * SALP_MAX_OBSTACLES)
@@ -224,6 +224,16 @@ int salp_collect(SalpEnv* h, const SalpPolicyRollout* r, void* stream);
  * -1 (default): sorted from 1 024 envs on.  Results per env are identical in
  * every mode. */
 int salp_set_lockstep_order(SalpEnv* h, int mode);
+
+/* Kernel of the chained calls (salp_rollout, salp_collect, salp_step_random
+ * from 32 env-steps on; ABI 9).  mode 0: one env per lane (k_rollout); 1: each
+ * env on two waves that split its physics tick and meet once per tick through
+ * LDS (k_rollout_pair: twice the waves, so an env count that leaves SIMDs idle
+ * with one env per lane fills the chip); -1 (default): the pair kernel while
+ * n_envs <= 128 x compute units.  The pair kernel has no randomised instance:
+ * with a randomisation switch on the chained calls use k_rollout.  Results per
+ * env are identical in every mode. */
+int salp_set_rollout_kernel(SalpEnv* h, int mode);
 
 /* GAE / returns over a rollout buffer: stable_baselines3's
  * RolloutBuffer.compute_returns_and_advantage (stable-baselines3 >= 2.0,

@@ -1,0 +1,171 @@
+"""k_rollout_pair (salp_pair.h): every env's physics tick split over two waves
+that meet once per tick through LDS.  It must give every env exactly the
+results of the one-env-per-lane k_rollout (and so of the oracle):
+
+* rollouts with a per-env step cap (each env ends at the same env-step
+  boundary whatever the scheduling) on both kernels: state, rollout buffers
+  and step counts bit for bit, odd env counts included (empty seats);
+* the same work cut into many short launches (chunk and launch boundaries in
+  the middle of cycles);
+* salp_collect (policy in the loop) on both kernels: every PPO buffer;
+* BASELINE configs[4]'s collection size, 32 768 envs: sampled envs of a
+  salp_collect run replayed from their start state on the C oracle with the
+  buffer's clipped actions (observations, rewards, episode starts, final
+  state bit for bit).
+"""
+import numpy as np
+import pytest
+import torch
+
+from grasp_lab_salp_amd._abi import FIELD, default_params
+from grasp_lab_salp_amd.batched_env import BatchedSalpEnv
+from grasp_lab_salp_amd.ppo import DIVERGED_OBS_ABS, DIVERGED_REWARD_ABS, ActorCritic, pack_policy
+from oracle.oracle import Oracle
+from oracle.sampled import _bits_differ
+
+pytestmark = pytest.mark.gpu
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def _same(a, b):
+    """Bit patterns equal, NaN payloads aside."""
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    if a.dtype.kind != "f":
+        return bool(np.array_equal(a, b))
+    iv = np.int64 if a.dtype == np.float64 else np.int32
+    return bool(np.all((a.view(iv) == b.view(iv)) | (np.isnan(a) & np.isnan(b))))
+
+
+def _rollout(kernel, n, seed, budgets, max_steps, cap=8, params=None):
+    env = BatchedSalpEnv(n, params=params or default_params(), seed=seed)
+    env.set_rollout_kernel(kernel)
+    od = env.obs_dim
+    z = lambda *s: torch.full(s, -5.0, dtype=torch.float32, device="cuda")  # noqa: E731
+    bufs = {"obs": z(cap, n, od), "obs_before": z(cap, n, od), "actions": z(cap, n, 3), "rewards": z(cap, n),
+            "dones": torch.full((cap, n), 7, dtype=torch.uint8, device="cuda")}
+    done = torch.zeros(n, dtype=torch.int64, device="cuda")
+    for b in budgets:
+        env.rollout(b, buffers=bufs, steps_done=done, max_steps=max_steps)
+    torch.cuda.synchronize()
+    out = {"state": _np(env.get_state()), "steps": _np(done), **{k: _np(v) for k, v in bufs.items()}}
+    env.close()
+    return out
+
+
+@pytest.mark.parametrize("n", [1, 200, 4096, 32768])
+def test_pair_rollout_equals_single_lane_rollout(n):
+    steps = 6 if n <= 4096 else 3
+    a = _rollout(0, n, 11, [10 ** 7], steps)
+    b = _rollout(1, n, 11, [10 ** 7], steps)
+    assert (a["steps"] == steps).all() and (b["steps"] == steps).all()
+    for k in a:
+        assert _same(a[k], b[k]), k
+
+
+def test_pair_rollout_cut_into_short_launches():
+    """97-tick launches (chunk 128) end in the middle of cycles and chunks."""
+    n = 1000
+    one = _rollout(1, n, 5, [10 ** 7], 5)
+    cut = _rollout(1, n, 5, [97] * 400 + [10 ** 7], 5)
+    for k in one:
+        assert _same(one[k], cut[k]), k
+
+
+def test_pair_rollout_with_timeouts_and_zero_obstacles():
+    p = default_params(num_obstacles=0)
+    p.max_cycles = 3
+    a = _rollout(0, 777, 3, [10 ** 7], 7, params=p)
+    b = _rollout(1, 777, 3, [10 ** 7], 7, params=p)
+    for k in a:
+        assert _same(a[k], b[k]), k
+
+
+def _policy(seed, obs_dim):
+    torch.manual_seed(seed)
+    pol = ActorCritic(obs_dim, 3).cuda()
+    with torch.no_grad():
+        pol.action_net.weight.mul_(60.0)   # actions spread over the box
+        pol.log_std.copy_(torch.tensor([-0.7, -0.4, -0.2]))
+    return pol
+
+
+def _collect(kernel, n, n_steps, seed=23, max_cycles=500, pol_seed=1):
+    p = default_params()
+    p.max_cycles = max_cycles
+    env = BatchedSalpEnv(n, params=p, seed=seed)
+    env.set_rollout_kernel(kernel)
+    obs0 = env.reset()
+    start = _np(env.get_state())
+    w = pack_policy(_policy(pol_seed, env.obs_dim))
+    z = lambda *s: torch.full(s, -7.0, dtype=torch.float32, device="cuda")  # noqa: E731
+    bufs = {"obs": z(n_steps, n, env.obs_dim), "actions": z(n_steps, n, 3), "rewards": z(n_steps, n),
+            "episode_starts": z(n_steps, n), "values": z(n_steps, n), "log_probs": z(n_steps, n)}
+    ep_start = torch.ones(n, dtype=torch.float32, device="cuda")
+    last_obs = obs0.clone()
+    ep_stats = torch.zeros(4, dtype=torch.float64, device="cuda")
+    diverged = torch.zeros(1, dtype=torch.int64, device="cuda")
+    env.collect(w, n_steps, bufs, ep_start, last_obs, ep_stats, diverged, noise_seed=99, gamma=0.99,
+                diverged_obs_abs=DIVERGED_OBS_ABS, diverged_reward_abs=DIVERGED_REWARD_ABS)
+    torch.cuda.synchronize()
+    out = {"state": _np(env.get_state()), "ep_start": _np(ep_start), "last_obs": _np(last_obs),
+           "diverged": _np(diverged), "ep_stats": _np(ep_stats), **{k: _np(v) for k, v in bufs.items()}}
+    env.close()
+    return out, start, obs0
+
+
+@pytest.mark.parametrize("n,n_steps,max_cycles", [(500, 9, 3), (32768, 8, 500)])
+def test_pair_collect_equals_single_lane_collect(n, n_steps, max_cycles):
+    a, _, _ = _collect(0, n, n_steps, max_cycles=max_cycles)
+    b, _, _ = _collect(1, n, n_steps, max_cycles=max_cycles)
+    for k in a:
+        if k == "ep_stats":   # float64 atomics: the summation order follows the scheduling
+            assert np.allclose(a[k], b[k], rtol=1e-12, atol=0), (a[k], b[k])
+        else:
+            assert _same(a[k], b[k]), k
+
+
+def test_pair_collect_32768_envs_sampled_envs_replay_on_the_oracle():
+    """The auto choice at 32 768 envs is the pair kernel.  256 sampled env ids
+    (the first and last workgroup's seats included) are replayed on the C
+    oracle from their state before the call, stepping with the clipped actions
+    the kernel recorded, resetting where the kernel's divergence guard did
+    (the guard's own condition re-evaluated on the oracle's outputs), and the
+    recorded observations / rewards / episode starts and the final state must
+    be the oracle's bit for bit (float32 rewards: rows without a timeout
+    bootstrap)."""
+    n, T = 32768, 24
+    out, start, obs0 = _collect(-1, n, T)
+    p = default_params()
+    rng = np.random.default_rng(0)
+    ids = np.unique(np.concatenate([np.arange(64), np.arange(n - 64, n), rng.choice(n, 128, replace=False)]))
+    low, high = np.float32([0, 0, -1]), np.float32([1, 1, 1])
+    obs0 = _np(obs0)
+    for i in ids:
+        o = Oracle(p, 1, seed=23, env_offset=int(i))
+        o.state[:, 0] = start[:, i]
+        obs = obs0[i].copy()
+        for t in range(T):
+            assert not _bits_differ(out["obs"][t, i], obs).any(), (i, t)
+            a = np.clip(out["actions"][t, i], low, high)[None]
+            r = o.step(a, auto_reset=True)
+            done = bool(r["terminated"][0] or r["truncated"][0])
+            last = r["terminal_obs"][0] if done else r["obs"][0]
+            bad = not (abs(r["reward"][0]) <= DIVERGED_REWARD_ABS) or not np.all(np.abs(last) <= DIVERGED_OBS_ABS)
+            if bad:
+                assert out["rewards"][t, i] == 0.0
+                if not done:
+                    obs = o.reset(np.ones(1, np.uint8))[0]
+                else:
+                    obs = r["obs"][0]
+            else:
+                if not (r["truncated"][0] and not r["terminated"][0]):
+                    assert not _bits_differ(out["rewards"][t, i:i + 1], np.float32(r["reward"][:1])).any(), (i, t)
+                obs = r["obs"][0]
+            if t + 1 < T:
+                assert out["episode_starts"][t + 1, i] == (1.0 if (done or bad) else 0.0), (i, t)
+        assert not _bits_differ(out["last_obs"][i], obs).any(), i
+        diff = _bits_differ(out["state"][:, i], o.state[:, 0])
+        assert not diff.any(), (i, [f for f, k in FIELD.items() if diff[k]])
