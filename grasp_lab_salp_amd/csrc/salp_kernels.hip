@@ -764,7 +764,7 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
 // k_rollout.
 constexpr int kPairEnvs = 128;
 constexpr int kXchAB = 5;    // A -> B: v x (M_a v) (3), jet torque y, z
-constexpr int kXchBA = 12;   // B -> A: w (3), alpha y, z, sin/cos roll, pitch (4), yaw, drag-force coefficients (2)
+constexpr int kXchBA = 13;   // B -> A: w (3), alpha y, z, sin/cos of roll, pitch, yaw (6), drag-force coefficients (2)
 constexpr int kXchBase = 4 * kXchAB * 64;                           // first double of the B -> A packets
 constexpr int kXchDoubles = kXchBase + 4 * kXchBA * 64;
 static_assert(kXchDoubles <= salp::SPILL_N * kPairEnvs, "the packets live in the spill slots' LDS");
@@ -780,7 +780,7 @@ __device__ unsigned int g_pair_timeouts;
 #ifndef SALP_PAIR_PROF
 #define SALP_PAIR_PROF 0
 #endif
-enum { PP_BOUNDARY, PP_TICK, PP_PUBLISH, PP_WAIT, PP_READ, PP_WORLD, PP_N };
+enum { PP_BOUNDARY, PP_TICK, PP_PUBLISH, PP_WAIT, PP_READ, PP_WORLD, PP_BARRIER, PP_N };
 __device__ unsigned long long g_pair_prof[2][PP_N];
 struct PairProf {
     unsigned long long acc[PP_N] = {};
@@ -950,7 +950,9 @@ __device__ __forceinline__ void pair_wave_a(PairShared& sh, const RolloutArgs& A
             sh.mask[b][grp] = ballot;
             sh.amask[b][grp] = aballot;
         }
+        prof.lap(PP_BOUNDARY);
         __syncthreads();   // #1
+        prof.lap(PP_BARRIER);
         pair_reseat(sh, b, seat, s, steps, pending, active, all_done);
         i = base + s;
         if (all_done) continue;
@@ -959,7 +961,9 @@ __device__ __forceinline__ void pair_wave_a(PairShared& sh, const RolloutArgs& A
         salp::HotA h;
         salp::unspill_a(h, ns);
         if (!active) h.b2 = -INFINITY;
+        prof.lap(PP_BOUNDARY);
         __syncthreads();   // #2: slots read; the packets may overwrite them now
+        prof.lap(PP_BARRIER);
         {
             const Params PV = salp::pin_params(P);
             const int chunk = A.chunk, q8 = A.steady_q8;
@@ -995,8 +999,8 @@ __device__ __forceinline__ void pair_wave_a(PairShared& sh, const RolloutArgs& A
                 prof.lap(PP_WAIT);
                 const double* const q = ba + (rcv & 1) * kXchBA * 64;
                 h.w0 = q[0 * 64]; h.w1 = q[1 * 64]; h.w2 = q[2 * 64]; h.al1 = q[3 * 64]; h.al2 = q[4 * 64];
-                h.sp = q[5 * 64]; h.cp = q[6 * 64]; h.st = q[7 * 64]; h.cth = q[8 * 64]; h.e2 = q[9 * 64];
-                h.kc0 = q[10 * 64]; h.kc1 = q[11 * 64];
+                h.sp = q[5 * 64]; h.cp = q[6 * 64]; h.st = q[7 * 64]; h.cth = q[8 * 64]; h.ss = q[9 * 64];
+                h.cs = q[10 * 64]; h.kc0 = q[11 * 64]; h.kc1 = q[12 * 64];
                 ++rcv;
                 prof.lap(PP_READ);
             };
@@ -1004,28 +1008,37 @@ __device__ __forceinline__ void pair_wave_a(PairShared& sh, const RolloutArgs& A
             int mode = decide();
             publish(mode);
             recv();
+            // pend: the lane's last tick still owes its world-frame position
+            // update (step_a does it at the start of the next tick, with the
+            // roll / pitch / yaw the partner sent after that tick)
+            bool pend = false;
             while (mode != salp::PM_END && ok) {
                 const bool ticks = h.ct < h.b2;
                 if (mode == salp::PM_FULL) {
-                    if (ticks) salp::tick_a<salp::PM_FULL>(h, PV, c32);
+                    if (ticks) salp::step_a<salp::PM_FULL>(h, PV, c32, pend);
                 } else if (mode == salp::PM_STEADY) {
                     bool settled = true;
-                    if (ticks) settled = salp::tick_a<salp::PM_STEADY>(h, PV, c32);
+                    if (ticks) settled = salp::step_a<salp::PM_STEADY>(h, PV, c32, pend);
                     if (__all(settled)) stage = 2;
                 } else {
-                    if (ticks) salp::tick_a<salp::PM_SETTLED>(h, PV, c32);
+                    if (ticks) salp::step_a<salp::PM_SETTLED>(h, PV, c32, pend);
                 }
+                pend = pend || ticks;
                 mode = decide();
                 prof.lap(PP_TICK);
                 publish(mode);
                 recv();
-                if (ticks) salp::a_world(h, PV);
-                prof.lap(PP_WORLD);
             }
+            if (pend) salp::a_world(h, PV);
+            prof.lap(PP_WORLD);
         }
+        prof.lap(PP_BOUNDARY);
         __syncthreads();   // #3: packets done
+        prof.lap(PP_BARRIER);
         salp::spill_a(h, ns, P);
+        prof.lap(PP_BOUNDARY);
         __syncthreads();   // #4: slots whole again
+        prof.lap(PP_BARRIER);
     }
 }
 
@@ -1055,7 +1068,9 @@ __device__ __forceinline__ void pair_wave_b(PairShared& sh, const RolloutArgs& A
             return;
         }
         const int b = (int)(c & 1);
+        prof.lap(PP_BOUNDARY);
         __syncthreads();   // #1
+        prof.lap(PP_BARRIER);
         pair_reseat(sh, b, seat, s, steps, pending, active, all_done);
         if (all_done) continue;
         const salp::SpillSlot ns{sh.big + s, kPairEnvs};
@@ -1063,7 +1078,9 @@ __device__ __forceinline__ void pair_wave_b(PairShared& sh, const RolloutArgs& A
         salp::HotB h;
         salp::unspill_b(h, ns, P);
         if (!active) h.b2 = -INFINITY;
+        prof.lap(PP_BOUNDARY);
         __syncthreads();   // #2
+        prof.lap(PP_BARRIER);
         {
             const Params PV = salp::pin_params(P);
             double* const ab = sh.big + grp * 2 * kXchAB * 64 + lane;
@@ -1071,8 +1088,8 @@ __device__ __forceinline__ void pair_wave_b(PairShared& sh, const RolloutArgs& A
             const auto publish = [&]() {
                 double* const o = ba + (pub & 1) * kXchBA * 64;
                 o[0 * 64] = h.w0; o[1 * 64] = h.w1; o[2 * 64] = h.w2; o[3 * 64] = h.al1; o[4 * 64] = h.al2;
-                o[5 * 64] = h.sp; o[6 * 64] = h.cp; o[7 * 64] = h.st; o[8 * 64] = h.cth; o[9 * 64] = h.e2;
-                o[10 * 64] = h.kc0; o[11 * 64] = h.kc1;
+                o[5 * 64] = h.sp; o[6 * 64] = h.cp; o[7 * 64] = h.st; o[8 * 64] = h.cth; o[9 * 64] = h.ss;
+                o[10 * 64] = h.cs; o[11 * 64] = h.kc0; o[12 * 64] = h.kc1;
                 pair_publish(&sh.cnt[grp][1], ++pub);
             };
             // a bound on the ticks of one chunk (A ends it earlier)
@@ -1090,18 +1107,22 @@ __device__ __forceinline__ void pair_wave_b(PairShared& sh, const RolloutArgs& A
                 prof.lap(PP_READ);
                 if (mode == salp::PM_END || !ok) break;
                 if (h.ct < h.b2) {
-                    if (mode == salp::PM_FULL) salp::tick_b<salp::PM_FULL>(h, PV, c32);
-                    else if (mode == salp::PM_STEADY) salp::tick_b<salp::PM_STEADY>(h, PV, c32);
-                    else salp::tick_b<salp::PM_SETTLED>(h, PV, c32);
+                    if (mode == salp::PM_FULL) salp::step_b<salp::PM_FULL>(h, PV, c32);
+                    else if (mode == salp::PM_STEADY) salp::step_b<salp::PM_STEADY>(h, PV, c32);
+                    else salp::step_b<salp::PM_SETTLED>(h, PV, c32);
                 }
                 prof.lap(PP_TICK);
                 publish();
                 prof.lap(PP_PUBLISH);
             }
         }
+        prof.lap(PP_BOUNDARY);
         __syncthreads();   // #3
+        prof.lap(PP_BARRIER);
         salp::spill_b(h, ns);
+        prof.lap(PP_BOUNDARY);
         __syncthreads();   // #4
+        prof.lap(PP_BARRIER);
     }
 }
 
@@ -1292,6 +1313,18 @@ int32_t rollout_steady_q8() {
     }();
     return q;
 }
+// The same budget for k_rollout_pair, whose steady ticks cost relatively more
+// (the per-tick packet exchange is the same for every kind of tick): q = 380
+// (32 768 envs, profiles/r4_experiments.md r4h: 300 / 380 / 480 x chunk
+// 256 / 384 / 512).  SALP_PAIR_STEADY_Q8 overrides it.
+int32_t pair_steady_q8() {
+    static const int32_t q = [] {
+        const char* e = std::getenv("SALP_PAIR_STEADY_Q8");
+        const long v = e ? std::strtol(e, nullptr, 10) : 0;
+        return (int32_t)(v > 0 && v < (1 << 16) ? v : 380);
+    }();
+    return q;
+}
 
 // Any randomisation switch on: launch the RAND instantiation of the kernels.
 bool randomized(const Params& d) { return d.rand_dyn || d.rand_dist || d.rand_act || d.rand_obs || d.latency; }
@@ -1317,8 +1350,10 @@ unsigned pair_blocks_for(int64_t n) { return (unsigned)((n + kPairEnvs - 1) / kP
 // One chained launch on the kernel use_pair chooses.
 int launch_chained(SalpEnv* h, const RolloutArgs& args, bool pol, hipStream_t st, const char* what) {
     if (use_pair(h)) {
+        RolloutArgs pa = args;
+        pa.steady_q8 = pair_steady_q8();
         hipLaunchKernelGGL(pol ? k_rollout_pair<true> : k_rollout_pair<false>, dim3(pair_blocks_for(h->n)),
-                           dim3(kBlock), 0, st, args);
+                           dim3(kBlock), 0, st, pa);
     } else if (pol) {
         hipLaunchKernelGGL((randomized(h->dp) ? k_rollout<true, true> : k_rollout<false, true>),
                            dim3(blocks_for(h->n)), dim3(kBlock), 0, st, args);

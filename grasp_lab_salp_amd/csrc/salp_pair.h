@@ -47,14 +47,14 @@ struct HotA {
     double m, rm, mr, speed;                 /* mass-side geometry (+ 1/m) */
     double amv0, amv1, amv2, jf0, jf1, jf2;  /* this tick's (M_a v) and jet force, prepared */
     /* from wave B: state after the previous tick */
-    double w0, w1, w2, al1, al2, sp, cp, st, cth, e2, kc0, kc1;
+    double w0, w1, w2, al1, al2, sp, cp, st, cth, ss, cs, kc0, kc1;
     int phase;
     bool g32, pv32, c32;
 };
 /* wave B's state of one env */
 struct HotB {
     double w0, w1, w2, al0, al1, al2, e0, e1, e2, g0, g1, g2, pI0, pI1, pI2;
-    double sp, cp, st, cth;
+    double sp, cp, st, cth, ss, cs;   /* sin/cos of roll, pitch (and yaw, for wave A) */
     double L, W, ct, refill, c, cr, rr, mx, b1, b2;
     double I0, I1, rI0, rI1, ra0, ra1, dimx, dimy, kc0, kc1;
     /* from wave A: this tick's v x (M_a v) and jet torque y, z */
@@ -103,34 +103,103 @@ SD void pair_clock(double& ct, int& phase, double b1, double b2, double mx) {
     }
 }
 
-/* Wave A's part of one tick (MODE: PM_FULL / PM_STEADY / PM_SETTLED).  Returns,
- * for a steady tick, whether the lane is settled after it (tick()). */
+/* The world-frame position update of the tick just done (tick()'s
+ * to_world_frame_jit block): yaw sin/cos, R at the new angles (roll / pitch
+ * sin/cos from wave B), p += (R v) dt. */
+SD void a_world(HotA& h, const Params&) {
+    const Rot R = rot_sc(h.sp, h.cp, h.st, h.cth, h.ss, h.cs);
+    double vw[3];
+    rot_apply(R, h.v0, h.v1, h.v2, vw);
+    h.p0 = sm_mad(vw[0], DT, h.p0); h.p1 = sm_mad(vw[1], DT, h.p1); h.p2 = sm_mad(vw[2], DT, h.p2);
+}
+
+/* ---------------------------------------------- the scheduled ticks */
+/* Each wave's part of a tick is scheduled for instruction-level parallelism: with one wave per SIMD a wave is issue-bound only while it has
+ * independent work between dependent instructions, and half a tick is a few
+ * long dependence chains.  step_a / step_b compute the same values in one
+ * basic block per tick kind: wave A interleaves the previous tick's
+ * world-frame update (yaw sin/cos, R v), this tick's clock / phase / mass-side
+ * geometry and Newton's equations (the geometry into temporaries, committed
+ * after Newton, which reads the tick-start values); wave B its shape-side
+ * geometry with Euler's equations, and both roll / pitch sin/cos on one
+ * straight path when every ticking lane's angles are small, then the yaw's
+ * for wave A.  Every value is the expression tick() computes. */
+
+/* sm_sincos_p of two angles; one straight-line path when every active lane
+ * takes the |x| <= pi/4 (or NaN) arm of both. */
+SD void sincos2_p(double x0, double x1, double* s0, double* c0, double* s1, double* c1, SmPoly K) {
+    const bool small0 = (sm_hi(x0) & 0x7fffffff) <= 0x3fe921fb || x0 != x0;
+    const bool small1 = (sm_hi(x1) & 0x7fffffff) <= 0x3fe921fb || x1 != x1;
+    if (__all(small0 && small1)) {
+        *s0 = sm_ksin_p(x0, 0.0, 0, K);
+        *c0 = sm_kcos_p(x0, 0.0, K);
+        *s1 = sm_ksin_p(x1, 0.0, 0, K);
+        *c1 = sm_kcos_p(x1, 0.0, K);
+    } else {
+        sm_sincos_p(x0, s0, c0, K);
+        sm_sincos_p(x1, s1, c1, K);
+    }
+}
+
+/* The world-frame update owed for the previous tick (pend: it ticked), then
+ * this tick.  Returns, for a steady tick, whether the lane is settled. */
 template <int MODE>
-SD bool tick_a(HotA& h, const Params& P, Cache32 c32) {
+SD bool step_a(HotA& h, const Params& P, Cache32 c32, bool pend) {
     constexpr bool STEADY = MODE != PM_FULL, SETTLED = MODE == PM_SETTLED;
+    {   /* a_world of the previous tick, with v before this tick's Newton */
+        const Rot R = rot_sc(h.sp, h.cp, h.st, h.cth, h.ss, h.cs);
+        double vw[3];
+        rot_apply(R, h.v0, h.v1, h.v2, vw);
+        const double p0 = sm_mad(vw[0], DT, h.p0), p1 = sm_mad(vw[1], DT, h.p1), p2 = sm_mad(vw[2], DT, h.p2);
+        h.p0 = pend ? p0 : h.p0;
+        h.p1 = pend ? p1 : h.p1;
+        h.p2 = pend ? p2 : h.p2;
+    }
+    /* clock, phase and (full ticks) the mass-side geometry of this tick */
+    double ct = h.ct;
+    int phase = h.phase;
+    pair_clock<STEADY>(ct, phase, h.b1, h.b2, h.mx);
+    double L = h.L, W = h.W, V = h.V, com = h.com, comr = h.comr, coma = h.coma, mn = h.m, mr = h.mr, sp = h.speed,
+           rmn = h.rm;
+    bool f = h.g32;
+    if (!STEADY) {
+        body_lw(P, phase, ct, h.refill, h.mx, h.c, h.cr, h.rr, h.c32, &L, &W, &f);
+        const Core c = core(L, W, false);
+        V = water_volume(P, c, false);
+        double wm = water_mass(P, V, false);
+        com = center_of_mass(P, c, wm, false);
+        mn = geo_mass(P, wm, false);
+        if (f) {
+            V = c32[C32_V]; wm = c32[C32_WM]; com = c32[C32_COM]; mn = c32[C32_M];
+        }
+        comr = div_dt(com - h.com);
+        coma = div_dt(comr - h.comr);
+        Geo ng;
+        ng.m = mn;
+        jet_rates(P, V, h.V, wm, f, h.g32, ng);   /* pV <- V, pv32 <- g32 first (tick()) */
+        mr = ng.mr;
+        sp = ng.speed;
+        rmn = rcp_of(mn).r;
+    }
+    /* Newton's equations with the tick-start values */
     const double m = h.m;
-    /* Coriolis force -w x (M v) (src/dynamics.py:159-162) */
     double mv0 = m * h.v0, mv1 = m * h.v1, mv2 = m * h.v2;
     double cf0 = -cross_c(h.w1, mv2, h.w2, mv1), cf1 = -cross_c(h.w2, mv0, h.w0, mv2),
            cf2 = -cross_c(h.w0, mv1, h.w1, mv0);
-    /* drag force (src/dynamics.py:110-116) */
     double vn = np_norm3(h.v0, h.v1, h.v2);
     double df0 = sm_mad(h.kc0 * h.v0, DRAG_FORCE_RATIO, h.kc0 * vn * h.v0);
     double df1 = sm_mad(h.kc1 * h.v1, DRAG_FORCE_RATIO, h.kc1 * vn * h.v1);
     double df2 = sm_mad(h.kc1 * h.v2, DRAG_FORCE_RATIO, h.kc1 * vn * h.v2);
-    /* added-mass force (src/dynamics.py:131-141); M_a v prepared */
-    const double mr = SETTLED ? 0.0 : h.mr;
+    const double mrt = SETTLED ? 0.0 : h.mr;
     double am0 = m * AMF0, am1 = m * AMF1, am2 = m * AMF2;
-    double amr0 = mr * AMRF, amr1 = mr * AMRF, amr2 = mr * AMRF;
+    double amr0 = mrt * AMRF, amr1 = mrt * AMRF, amr2 = mrt * AMRF;
     double af0 = -sm_mad(amr0, h.v0, sm_mad(am0, h.a0, cross_c(h.w1, h.amv2, h.w2, h.amv1)));
     double af1 = -sm_mad(amr1, h.v1, sm_mad(am1, h.a1, cross_c(h.w2, h.amv0, h.w0, h.amv2)));
     double af2 = -sm_mad(amr2, h.v2, sm_mad(am2, h.a2, cross_c(h.w0, h.amv1, h.w1, h.amv0)));
-    /* fictitious forces of the moving centre of mass (src/robot.py:806-810) */
     const double cx = h.com, crx = SETTLED ? 0.0 : h.comr;
     double acc_y = (h.w0 * (h.w1 * cx) + (h.w2 * crx) * 2.0) + h.al2 * cx;
     double acc_z = (h.w0 * (h.w2 * cx) + -(h.w1 * crx) * 2.0) + -(h.al1 * cx);
     double acc_x = cross_c(h.w1, -(h.w1 * cx), h.w2, h.w2 * cx) + (SETTLED ? 0.0 : h.coma);
-    /* total force and linear acceleration (src/dynamics.py:5-10) */
     const Rcp rm{m, h.rm};
     const double na0 = qdiv(sm_mad(acc_x, m, ((h.jf0 + df0) + af0) + cf0), rm);
     const double na1 = qdiv(sm_mad(acc_y, m, ((h.jf1 + df1) + af1) + cf1), rm);
@@ -138,22 +207,22 @@ SD bool tick_a(HotA& h, const Params& P, Cache32 c32) {
     h.a0 = na0; h.a1 = na1; h.a2 = na2;
     h.v0 = sm_mad(na0, DT, h.v0); h.v1 = sm_mad(na1, DT, h.v1); h.v2 = sm_mad(na2, DT, h.v2);
     h.q0 = sm_mad(h.v0, DT, h.q0); h.q1 = sm_mad(h.v1, DT, h.q1); h.q2 = sm_mad(h.v2, DT, h.q2);
-    /* clocks, phase, properties */
-    pair_clock<STEADY>(h.ct, h.phase, h.b1, h.b2, h.mx);
+    /* commit the tick's clock and properties */
+    h.ct = ct;
+    h.phase = phase;
     h.time += DT;
     h.pV = h.V;
     if (STEADY) {
         h.pv32 = false;
-        /* the steady tail of tick() (see there) */
         if (SETTLED) return true;
         const auto zero = [&] {
             return (__double_as_longlong(h.comr) | __double_as_longlong(h.coma) | __double_as_longlong(h.mr) |
                     __double_as_longlong(h.speed)) == 0;
         };
         if (!__all(zero())) {
-            const double comr = div_dt(h.com - h.com);
-            h.coma = div_dt(comr - h.comr);
-            h.comr = comr;
+            const double cr = div_dt(h.com - h.com);
+            h.coma = div_dt(cr - h.comr);
+            h.comr = cr;
             const double pwm = r32(sel(h.pv32, P.density) * h.pV, h.pv32);
             h.mr = div_dt(water_mass(P, h.V, false) - pwm);
             h.speed = qdiv(div_dt(h.V - h.pV), rcp_of(P.nozzle_area));
@@ -161,82 +230,63 @@ SD bool tick_a(HotA& h, const Params& P, Cache32 c32) {
         return zero();
     }
     h.pv32 = h.g32;
-    bool f;
-    body_lw(P, h.phase, h.ct, h.refill, h.mx, h.c, h.cr, h.rr, h.c32, &h.L, &h.W, &f);
-    h.g32 = f;
-    /* update_properties, mass side (float64, or the cycle's float32 values) */
-    const Core c = core(h.L, h.W, false);
-    double V = water_volume(P, c, false);
-    double wm = water_mass(P, V, false);
-    double com = center_of_mass(P, c, wm, false);
-    double mn = geo_mass(P, wm, false);
-    if (f) {
-        V = c32[C32_V]; wm = c32[C32_WM]; com = c32[C32_COM]; mn = c32[C32_M];
-    }
-    h.V = V;
-    const double comr = div_dt(com - h.com);
-    h.coma = div_dt(comr - h.comr);
-    h.com = com;
-    h.comr = comr;
-    Geo ng;
-    ng.m = mn;
-    jet_rates(P, V, h.pV, wm, f, h.pv32, ng);
-    h.m = mn;
-    h.mr = ng.mr;
-    h.speed = ng.speed;
-    h.rm = rcp_of(mn).r;
+    h.L = L; h.W = W; h.g32 = f;
+    h.V = V; h.com = com; h.comr = comr; h.coma = coma;
+    h.m = mn; h.mr = mr; h.speed = sp; h.rm = rmn;
     return false;
 }
 
-/* The world-frame position update of the tick just done (tick()'s
- * to_world_frame_jit block): yaw sin/cos, R at the new angles (roll / pitch
- * sin/cos from wave B), p += (R v) dt. */
-SD void a_world(HotA& h, const Params& P) {
-    double ss, cs;
-    sm_sincos_nb_p(h.e2, &ss, &cs, P.sk);
-    const Rot R = rot_sc(h.sp, h.cp, h.st, h.cth, ss, cs);
-    double vw[3];
-    rot_apply(R, h.v0, h.v1, h.v2, vw);
-    h.p0 = sm_mad(vw[0], DT, h.p0); h.p1 = sm_mad(vw[1], DT, h.p1); h.p2 = sm_mad(vw[2], DT, h.p2);
-}
-
-/* Wave B's part of one tick. */
 template <int MODE>
-SD void tick_b(HotB& h, const Params& P, Cache32 c32) {
+SD void step_b(HotB& h, const Params& P, Cache32 c32) {
     constexpr bool STEADY = MODE != PM_FULL, SETTLED = MODE == PM_SETTLED;
+    /* clock, phase and (full ticks) the shape-side geometry of this tick */
+    double ct = h.ct;
+    int phase = h.phase;
+    pair_clock<STEADY>(ct, phase, h.b1, h.b2, h.mx);
+    double L = h.L, W = h.W;
+    bool f = h.g32;
+    Geo ng;
+    if (!STEADY) {
+        body_lw(P, phase, ct, h.refill, h.mx, h.c, h.cr, h.rr, h.c32, &L, &W, &f);
+        const Core c = core(L, W, false);
+        geo_shape(P, c, L, W, false, ng);
+        if (f) {
+            ng.I0 = c32[C32_I0]; ng.I1 = c32[C32_I1];
+            ng.kc0 = c32[C32_KC0]; ng.kc1 = c32[C32_KC1]; ng.ra0 = c32[C32_RA0]; ng.ra1 = c32[C32_RA1];
+            ng.dimx = c32[C32_DIMX]; ng.dimy = c32[C32_DIMY];
+        }
+        ng.rI0 = rcp_of(ng.I0).r;
+        ng.rI1 = rcp_of(ng.I1).r;
+    }
+    /* Euler's equations with the tick-start values */
     const double I0 = h.I0, I1 = h.I1;
-    /* Coriolis torque -w x (I w) (src/dynamics.py:165-168) */
     double iw0 = I0 * h.w0, iw1 = I1 * h.w1, iw2 = I1 * h.w2;
     double ct0 = -cross_c(h.w1, iw2, h.w2, iw1), ct1 = -cross_c(h.w2, iw0, h.w0, iw2),
            ct2 = -cross_c(h.w0, iw1, h.w1, iw0);
-    /* drag torque (src/dynamics.py:119-128) */
     double wn = np_norm3(h.w0, h.w1, h.w2);
     double dt0 = sm_mad(h.ra0 * h.w0 * h.W, DRAG_TORQUE_RATIO, h.ra0 * wn * h.w0 * h.dimx);
     double dt1 = sm_mad(h.ra1 * h.w1 * h.W, DRAG_TORQUE_RATIO, h.ra1 * wn * h.w1 * h.dimy);
     double dt2 = sm_mad(h.ra1 * h.w2 * h.W, DRAG_TORQUE_RATIO, h.ra1 * wn * h.w2 * h.dimy);
-    /* deformation torque -(dI/dt) w; prev_I <- I (src/robot.py:888-896) */
     double ir0 = 0.0, ir1 = 0.0, ir2 = 0.0;
     if (!SETTLED) {
         ir0 = div_dt(I0 - h.pI0);
         ir1 = div_dt(I1 - h.pI1);
-        ir2 = ir1;
-        if (h.pI2 != h.pI1) ir2 = div_dt(I1 - h.pI2);
+        const double ir2b = div_dt(I1 - h.pI2);
+        ir2 = h.pI2 != h.pI1 ? ir2b : ir1;
         h.pI0 = I0; h.pI1 = I1; h.pI2 = I1;
     }
-    /* added-mass torque (src/dynamics.py:144-156); v x (M_a v) from wave A */
     double at0 = I0 * AMT0, at1 = I1 * AMT1, at2 = I1 * AMT2;
     double atw0 = at0 * h.w0, atw1 = at1 * h.w1, atw2 = at2 * h.w2;
     double amt0 = -(sm_mad(at0, h.al0, cross_c(h.w1, atw2, h.w2, atw1)) + h.X0);
     double amt1 = -(sm_mad(at1, h.al1, cross_c(h.w2, atw0, h.w0, atw2)) + h.X1);
     double amt2 = -(sm_mad(at2, h.al2, cross_c(h.w0, atw1, h.w1, atw0)) + h.X2);
-    /* total torque and angular acceleration (src/dynamics.py:13-17) */
     const Rcp rI0{I0, h.rI0}, rI1{I1, h.rI1};
     const double nal0 = qdiv(sm_mad(-ir0, h.w0, dt0 + ct0) + amt0, rI0);
     const double nal1 = qdiv(sm_mad(-ir1, h.w1, (h.jt1 + dt1) + ct1) + amt1, rI1);
     const double nal2 = qdiv(sm_mad(-ir2, h.w2, (h.jt2 + dt2) + ct2) + amt2, rI1);
     h.al0 = nal0; h.al1 = nal1; h.al2 = nal2;
     h.w0 = sm_mad(nal0, DT, h.w0); h.w1 = sm_mad(nal1, DT, h.w1); h.w2 = sm_mad(nal2, DT, h.w2);
-    {   /* to_euler_angle_rate_jit (src/dynamics.py:20-31) at the current angles */
+    {
         const Rcp rc = rcp_of(h.cth);
         double tt = qdiv(h.st, rc);
         double r0 = sm_fma(h.cp * tt, h.w2, h.w0 + (h.sp * tt) * h.w1);
@@ -244,28 +294,17 @@ SD void tick_b(HotB& h, const Params& P, Cache32 c32) {
         double r2 = sm_fma(qdiv(h.cp, rc), h.w2, qdiv(h.sp, rc) * h.w1);
         h.e0 = sm_mad(r0, DT, h.e0); h.e1 = sm_mad(r1, DT, h.e1); h.e2 = sm_mad(r2, DT, h.e2);
     }
-    sm_sincos_p(h.e0, &h.sp, &h.cp, P.sk);
-    sm_sincos_p(h.e1, &h.st, &h.cth, P.sk);
     h.g0 = sm_mad(h.w0, DT, h.g0); h.g1 = sm_mad(h.w1, DT, h.g1); h.g2 = sm_mad(h.w2, DT, h.g2);
-    pair_clock<STEADY>(h.ct, h.phase, h.b1, h.b2, h.mx);
-    if (STEADY) return;
-    bool f;
-    body_lw(P, h.phase, h.ct, h.refill, h.mx, h.c, h.cr, h.rr, h.c32, &h.L, &h.W, &f);
-    h.g32 = f;
-    /* update_properties, shape side */
-    const Core c = core(h.L, h.W, false);
-    Geo ng;
-    geo_shape(P, c, h.L, h.W, false, ng);
-    if (f) {
-        ng.I0 = c32[C32_I0]; ng.I1 = c32[C32_I1];
-        ng.kc0 = c32[C32_KC0]; ng.kc1 = c32[C32_KC1]; ng.ra0 = c32[C32_RA0]; ng.ra1 = c32[C32_RA1];
-        ng.dimx = c32[C32_DIMX]; ng.dimy = c32[C32_DIMY];
+    h.ct = ct;
+    h.phase = phase;
+    if (!STEADY) {
+        h.L = L; h.W = W; h.g32 = f;
+        h.I0 = ng.I0; h.I1 = ng.I1; h.rI0 = ng.rI0; h.rI1 = ng.rI1;
+        h.kc0 = ng.kc0; h.kc1 = ng.kc1; h.ra0 = ng.ra0; h.ra1 = ng.ra1;
+        h.dimx = ng.dimx; h.dimy = ng.dimy;
     }
-    h.I0 = ng.I0; h.I1 = ng.I1;
-    h.rI0 = rcp_of(ng.I0).r;
-    h.rI1 = rcp_of(ng.I1).r;
-    h.kc0 = ng.kc0; h.kc1 = ng.kc1; h.ra0 = ng.ra0; h.ra1 = ng.ra1;
-    h.dimx = ng.dimx; h.dimy = ng.dimy;
+    sincos2_p(h.e0, h.e1, &h.sp, &h.cp, &h.st, &h.cth, P.sk);
+    sm_sincos_nb_p(h.e2, &h.ss, &h.cs, P.sk);   /* yaw: wave A's world-frame update */
 }
 
 /* ---------------------------------------- LDS slot <-> the two waves */
@@ -329,7 +368,8 @@ SD void unspill_a(HotA& h, SpillSlot s) {
     h.w0 = s[SP_W]; h.w1 = s[SP_W + 1]; h.w2 = s[SP_W + 2];
     h.al1 = s[SP_AL + 1]; h.al2 = s[SP_AL + 2];
     h.sp = s[SP_SP]; h.cp = s[SP_CP]; h.st = s[SP_ST]; h.cth = s[SP_CTH];
-    h.e2 = s[SP_E + 2]; h.kc0 = s[SP_KC0]; h.kc1 = s[SP_KC1];
+    h.ss = 0.0; h.cs = 1.0;   /* the first packet brings the yaw's (no world update is owed yet) */
+    h.kc0 = s[SP_KC0]; h.kc1 = s[SP_KC1];
     cycle_bounds_of(h.refill, h.turn, h.jet, h.coast, &h.mx, &h.b1, &h.b2);
 }
 /* Wave B's fields; X / jt of the first tick from wave A's fields of the slot,
@@ -341,6 +381,7 @@ SD void unspill_b(HotB& h, SpillSlot s, const Params& P) {
     h.g0 = s[SP_G]; h.g1 = s[SP_G + 1]; h.g2 = s[SP_G + 2];
     h.pI0 = s[SP_PI]; h.pI1 = s[SP_PI + 1]; h.pI2 = s[SP_PI + 2];
     h.sp = s[SP_SP]; h.cp = s[SP_CP]; h.st = s[SP_ST]; h.cth = s[SP_CTH];
+    sm_sincos_nb_p(h.e2, &h.ss, &h.cs, P.sk);
     h.I0 = s[SP_I0]; h.I1 = s[SP_I1]; h.kc0 = s[SP_KC0]; h.kc1 = s[SP_KC1];
     h.ra0 = s[SP_RA0]; h.ra1 = s[SP_RA1]; h.dimx = s[SP_DIMX]; h.dimy = s[SP_DIMY];
     h.rI0 = rcp_of(h.I0).r;
