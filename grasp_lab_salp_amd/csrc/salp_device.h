@@ -148,6 +148,24 @@ SD float cubef(float x) {
     return r;
 }
 
+/* sm_sincos_p of two angles (a tick's roll and pitch): one wave-uniform test
+ * and one straight-line path when every active lane takes the |x| <= pi/4 (or
+ * NaN) arm of both, instead of two divergent if/else regions with a reduction
+ * path each.  Bit-identical to two sm_sincos_p calls. */
+SD void sincos2_p(double x0, double x1, double* s0, double* c0, double* s1, double* c1, SmPoly K) {
+    const bool small0 = (sm_hi(x0) & 0x7fffffff) <= 0x3fe921fb || x0 != x0;
+    const bool small1 = (sm_hi(x1) & 0x7fffffff) <= 0x3fe921fb || x1 != x1;
+    if (__all(small0 && small1)) {
+        *s0 = sm_ksin_p(x0, 0.0, 0, K);
+        *c0 = sm_kcos_p(x0, 0.0, K);
+        *s1 = sm_ksin_p(x1, 0.0, 0, K);
+        *c1 = sm_kcos_p(x1, 0.0, K);
+    } else {
+        sm_sincos_p(x0, s0, c0, K);
+        sm_sincos_p(x1, s1, c1, K);
+    }
+}
+
 /* Rotation R = Rz(psi) Ry(theta) Rx(phi) (src/dynamics.py:34-58) from the
  * dgemm-order product with its zeros removed. */
 struct Rot { double r[3][3]; };

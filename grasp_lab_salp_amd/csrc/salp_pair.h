@@ -125,22 +125,6 @@ SD void a_world(HotA& h, const Params&) {
  * straight path when every ticking lane's angles are small, then the yaw's
  * for wave A.  Every value is the expression tick() computes. */
 
-/* sm_sincos_p of two angles; one straight-line path when every active lane
- * takes the |x| <= pi/4 (or NaN) arm of both. */
-SD void sincos2_p(double x0, double x1, double* s0, double* c0, double* s1, double* c1, SmPoly K) {
-    const bool small0 = (sm_hi(x0) & 0x7fffffff) <= 0x3fe921fb || x0 != x0;
-    const bool small1 = (sm_hi(x1) & 0x7fffffff) <= 0x3fe921fb || x1 != x1;
-    if (__all(small0 && small1)) {
-        *s0 = sm_ksin_p(x0, 0.0, 0, K);
-        *c0 = sm_kcos_p(x0, 0.0, K);
-        *s1 = sm_ksin_p(x1, 0.0, 0, K);
-        *c1 = sm_kcos_p(x1, 0.0, K);
-    } else {
-        sm_sincos_p(x0, s0, c0, K);
-        sm_sincos_p(x1, s1, c1, K);
-    }
-}
-
 /* The world-frame update owed for the previous tick (pend: it ticked), then
  * this tick.  Returns, for a steady tick, whether the lane is settled. */
 template <int MODE>
