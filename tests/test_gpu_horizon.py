@@ -1,9 +1,9 @@
 """Parity at the bench's own horizon (BASELINE.json configs[2], the headline).
 
 The exact bench workload: 65 536 envs, tick budget 8 192 per launch, chunk
-128, the default steady budget (q = 360), a 16-slot rollout buffer, 25
+128, the default steady budget (q = 480), a 16-slot rollout buffer, 25
 launches (~310 env-steps per env: re-seating, steady ticks, settled waves,
-auto-resets and diverged envs all exercised).  Then ~800 sampled env ids
+auto-resets and diverged envs all exercised).  Then ~830 sampled env ids
 (the first and the last workgroup, up to 64 diverged envs, 256 random ones)
 are replayed from creation on the OpenMP oracle for exactly the env-steps
 each completed plus its in-flight cycle (oracle/sampled.py), and the device
