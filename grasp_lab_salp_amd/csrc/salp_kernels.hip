@@ -331,6 +331,7 @@ __device__ __forceinline__ void policy_noise(uint64_t seed, uint64_t env_id, uin
 // The env's action for observation o: a = mean + std z (unclipped, as SB3's
 // buffer holds it), V(o) and log N(a; mean, std) summed over the dims, in the
 // expression order of torch.distributions.Normal.log_prob.
+// value == nullptr: the value network is evaluated elsewhere (k_rollout_pair's B wave).
 __device__ __forceinline__ void policy_act(const SalpPolicyRollout& R, int obs_dim, const float* o, uint64_t env_id,
                                            uint64_t step, float a[3], float* value, float* logp) {
     const PolicyW w = (PolicyW)R.weights;
@@ -339,7 +340,7 @@ __device__ __forceinline__ void policy_act(const SalpPolicyRollout& R, int obs_d
     float mean[3];
     policy_mlp<3>(w, SALP_POLICY_PI_W1, SALP_POLICY_PI_B1, SALP_POLICY_PI_W2, SALP_POLICY_PI_B2, SALP_POLICY_ACT_W,
                   SALP_POLICY_ACT_B, x, mean);
-    *value = policy_value(w, x);
+    if (value) *value = policy_value(w, x);
     float z[3];
     policy_noise(R.noise_seed, env_id, step, z);
     float lp = 0.0f;
@@ -352,6 +353,18 @@ __device__ __forceinline__ void policy_act(const SalpPolicyRollout& R, int obs_d
     }
     *logp = lp;
 }
+
+// Where a salp_collect boundary's value-network evaluations run: in place
+// (k_rollout), or handed to the B wave of k_rollout_pair through LDS
+// (ValuesToPartner, defined with that kernel) while the A wave evaluates the
+// policy mean and starts the next env-step.
+struct ValuesInPlace {
+    static constexpr bool kDefer = false;
+    __device__ __forceinline__ void start_rep() {}
+    __device__ __forceinline__ void boot(const float*, int, float, int64_t) {}
+    __device__ __forceinline__ void value(const float*, int, int64_t) {}
+    __device__ __forceinline__ void publish() {}
+};
 
 // torch.clamp(a, low, high): NaN stays NaN
 __device__ __forceinline__ float clamp_box(float a, float lo, float hi) { return a < lo ? lo : (a > hi ? hi : a); }
@@ -366,12 +379,12 @@ __device__ __forceinline__ float clamp_box(float a, float lo, float hi) { return
 // is cut into launches and chunks changes nothing but the count of env-steps
 // a launch completes.  POL: the actions come from the policy of salp_collect
 // and the outputs go to its buffers (R).
-template <bool RAND, bool POL, class ST>
+template <bool RAND, bool POL, class ST, class VS = ValuesInPlace>
 __device__ __forceinline__ void rollout_boundary(Hot& h, ST S, const Params& P, int64_t i,
                                                  uint64_t env_id, bool& pending, bool& active,
                                                  int64_t& steps, int64_t max_steps,
                                                  const SalpRolloutBuffers& B, double* reward_sum,
-                                                 const SalpPolicyRollout& R, salp::Cache32 c32) {
+                                                 const SalpPolicyRollout& R, salp::Cache32 c32, VS vs = VS()) {
     // o: the env's current observation once this boundary has produced one
     // (after a finished step, or the reset obs after an episode end)
     float o[SALP_OBS_DIM_MAX];
@@ -380,6 +393,7 @@ __device__ __forceinline__ void rollout_boundary(Hot& h, ST S, const Params& P, 
     // a few rounds so that zero-tick cycles chain without waiting a chunk
     for (int rep = 0; rep < 4; ++rep) {
         const bool fin = active && pending && !(h.ct < h.b2);
+        vs.start_rep();
         if (fin) {
             SF(SALP_F_STEP_COUNT) = SF(SALP_F_STEP_COUNT) + 1.0;
             salp::StepOut r = salp::finish_step<RAND>(h, S, P, i, o, nullptr);
@@ -398,9 +412,13 @@ __device__ __forceinline__ void rollout_boundary(Hot& h, ST S, const Params& P, 
                     rew = 0.0f;
                     atomicAdd((unsigned long long*)R.diverged, 1ull);
                 } else if (r.truncated && !r.terminated) {
-                    float x[kPIN];
-                    policy_input(o, P.obs_dim, x);
-                    rew = rew + (float)R.gamma * policy_value((PolicyW)R.weights, x);
+                    if (VS::kDefer) {
+                        vs.boot(o, P.obs_dim, rew, (int64_t)steps);   // the partner writes rewards[row]
+                    } else {
+                        float x[kPIN];
+                        policy_input(o, P.obs_dim, x);
+                        rew = rew + (float)R.gamma * policy_value((PolicyW)R.weights, x);
+                    }
                 }
                 if (reset && !bad) {
                     atomicAdd(&R.ep_stats[0], SF(SALP_F_EP_RETURN));
@@ -408,7 +426,7 @@ __device__ __forceinline__ void rollout_boundary(Hot& h, ST S, const Params& P, 
                     if (r.terminated) atomicAdd(&R.ep_stats[2], 1.0);   // the target was reached
                     atomicAdd(&R.ep_stats[3], SF(SALP_F_EP_LEN));
                 }
-                R.rewards[row] = rew;
+                if (!(VS::kDefer && !bad && r.truncated && !r.terminated)) R.rewards[row] = rew;
                 reset = reset || bad;
                 ep_start = reset ? 1.0f : 0.0f;
                 R.episode_start[i] = ep_start;
@@ -437,7 +455,7 @@ __device__ __forceinline__ void rollout_boundary(Hot& h, ST S, const Params& P, 
             }
         }
         const bool beg = active && !pending;
-        if (beg) {
+        if (beg) {   // the observation the next action is taken on
             if (POL && !have_o) {
                 // first step of a salp_collect call: the observation the caller
                 // holds (last_obs is in/out: the previous call's last one, or the
@@ -452,17 +470,22 @@ __device__ __forceinline__ void rollout_boundary(Hot& h, ST S, const Params& P, 
                 salp::observation(h, Rt, S, P, i, o);
                 have_o = true;
             }
+            if (POL && VS::kDefer) vs.value(o, P.obs_dim, (int64_t)steps);
+        }
+        vs.publish();
+        if (beg) {
             float a[3];
             if (POL) {
                 if (!fin) ep_start = R.episode_start[i];
                 float raw[3], v, lp;
-                policy_act(R, P.obs_dim, o, env_id, (uint64_t)SF(SALP_F_STEP_COUNT), raw, &v, &lp);
+                policy_act(R, P.obs_dim, o, env_id, (uint64_t)SF(SALP_F_STEP_COUNT), raw, VS::kDefer ? nullptr : &v,
+                           &lp);
                 const size_t row = (size_t)steps * (size_t)P.n + (size_t)i;
                 for (int k = 0; k < P.obs_dim; ++k) R.obs[row * P.obs_dim + k] = o[k];
                 R.actions[row * 3 + 0] = raw[0];
                 R.actions[row * 3 + 1] = raw[1];
                 R.actions[row * 3 + 2] = raw[2];
-                R.values[row] = v;
+                if (!VS::kDefer) R.values[row] = v;
                 R.log_probs[row] = lp;
                 R.episode_starts[row] = ep_start;
                 a[0] = clamp_box(raw[0], 0.0f, 1.0f);
@@ -478,7 +501,11 @@ __device__ __forceinline__ void rollout_boundary(Hot& h, ST S, const Params& P, 
             salp::begin_step<RAND>(h, S, P, i, a[0], a[1], a[2], c32);
             pending = true;
         }
-        if (!fin && !beg) break;
+        if (VS::kDefer) {   // the partner follows rep by rep: the wave leaves together
+            if (!__any(fin || beg)) break;
+        } else if (!fin && !beg) {
+            break;
+        }
     }
 }
 
@@ -812,6 +839,23 @@ struct PairShared {
     uint8_t flags[kPairEnvs];
 };
 
+// salp_collect boundaries in k_rollout_pair: the A wave runs the env-steps and
+// the policy mean; the value-network evaluations (SB3's V(obs) of every new
+// step and gamma V(terminal obs) of a timeout's bootstrap) go to the B wave as
+// jobs, one LDS buffer per boundary round ("rep" of rollout_boundary), which
+// the B wave evaluates while the A wave goes on (ValuesToPartner).  Same
+// expressions, same results.
+struct PairJobs {
+    float boot_obs[4][kPIN][kPairEnvs];
+    float val_obs[4][kPIN][kPairEnvs];
+    float boot_rew[4][kPairEnvs];
+    int32_t boot_step[4][kPairEnvs];
+    int32_t val_step[4][kPairEnvs];
+    uint8_t flags[4][kPairEnvs];   // 1: bootstrap job, 2: value job
+    int cnt[2];                    // [group]: job buffers the A wave published
+    int done[2];                   // [group]: boundaries whose jobs are all published (chunk index + 1)
+};
+
 __device__ __forceinline__ bool pair_wait(int* flag, int target) {
     for (int it = 0; it < kPairSpin; ++it) {
         if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
@@ -822,6 +866,67 @@ __device__ __forceinline__ bool pair_wait(int* flag, int target) {
 }
 __device__ __forceinline__ void pair_publish(int* flag, int value) {
     __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+struct ValuesToPartner {
+    static constexpr bool kDefer = true;
+    PairJobs* J;
+    int grp, s, buf;
+    __device__ __forceinline__ void start_rep() {
+        buf = __hip_atomic_load(&J->cnt[grp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & 3;
+    }
+    __device__ __forceinline__ void boot(const float* o, int od, float rew, int64_t step) {
+        for (int k = 0; k < od; ++k) J->boot_obs[buf][k][s] = o[k];
+        J->boot_rew[buf][s] = rew;
+        J->boot_step[buf][s] = (int32_t)step;
+        J->flags[buf][s] |= 1;
+    }
+    __device__ __forceinline__ void value(const float* o, int od, int64_t step) {
+        for (int k = 0; k < od; ++k) J->val_obs[buf][k][s] = o[k];
+        J->val_step[buf][s] = (int32_t)step;
+        J->flags[buf][s] |= 2;
+    }
+    __device__ __forceinline__ void publish() {
+        const int c = __hip_atomic_load(&J->cnt[grp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        pair_publish(&J->cnt[grp], c + 1);
+    }
+};
+
+// The B wave's side: evaluate the published jobs of the boundary of chunk c
+// until the A wave marks it done.  `taken`: job buffers evaluated so far.
+__device__ __forceinline__ void pair_value_jobs(PairJobs& J, const RolloutArgs& A, int grp, int s, int64_t c,
+                                                int& taken) {
+    const PolicyW w = (PolicyW)A.R.weights;
+    const int64_t i = (int64_t)blockIdx.x * kPairEnvs + s;
+    const int od = A.P.obs_dim;
+    for (int it = 0; it < kPairSpin; ++it) {
+        const int pub = __hip_atomic_load(&J.cnt[grp], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (taken < pub) {
+            const int b = taken & 3;
+            const int f = J.flags[b][s];
+            if (f & 1) {
+                float x[kPIN];
+#pragma unroll
+                for (int k = 0; k < kPIN; ++k) x[k] = k < od ? J.boot_obs[b][k][s] : 0.0f;
+                const float rew = J.boot_rew[b][s] + (float)A.R.gamma * policy_value(w, x);
+                A.R.rewards[(size_t)J.boot_step[b][s] * (size_t)A.P.n + (size_t)i] = rew;
+            }
+            if (f & 2) {
+                float x[kPIN];
+#pragma unroll
+                for (int k = 0; k < kPIN; ++k) x[k] = k < od ? J.val_obs[b][k][s] : 0.0f;
+                A.R.values[(size_t)J.val_step[b][s] * (size_t)A.P.n + (size_t)i] = policy_value(w, x);
+            }
+            ++taken;
+            continue;
+        }
+        if (__hip_atomic_load(&J.done[grp], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= (int)(c + 1)) {
+            if (taken < __hip_atomic_load(&J.cnt[grp], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) continue;
+            return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_pair_timeouts, 1u);
 }
 
 // Position of the k-th set bit of the 128-bit mask m[0..1] (k < popcount).
@@ -879,7 +984,7 @@ __device__ __forceinline__ void pair_reseat(PairShared& sh, int b, int seat, int
 }
 
 template <bool POL>
-__device__ __forceinline__ void pair_wave_a(PairShared& sh, const RolloutArgs& A, int grp, int lane) {
+__device__ __forceinline__ void pair_wave_a(PairShared& sh, PairJobs* jobs, const RolloutArgs& A, int grp, int lane) {
     const Params& P = A.P;
     const int seat = grp * 64 + lane;
     const int64_t base = (int64_t)blockIdx.x * kPairEnvs;
@@ -900,6 +1005,10 @@ __device__ __forceinline__ void pair_wave_a(PairShared& sh, const RolloutArgs& A
         }
         salp::spill<false>(h, salp::SpillSlot{sh.big + s, kPairEnvs});
         if (lane < 2) sh.cnt[grp][lane] = 0;
+        if (POL && lane == 0) {
+            jobs->cnt[grp] = 0;
+            jobs->done[grp] = 0;
+        }
     }
     __syncthreads();   // #0
     int pub = 0, rcv = 0;
@@ -916,6 +1025,9 @@ __device__ __forceinline__ void pair_wave_a(PairShared& sh, const RolloutArgs& A
                                   &b1, &b2);
             need = active && (!pending || !(sl[salp::SP_CT] < b2));
         }
+        if (POL)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) jobs->flags[b][s] = 0;
         if (need) {
             const RolloutArgs a = fresh_args();
             const uint64_t env_id = (uint64_t)(a.P.env_offset + i);
@@ -923,11 +1035,17 @@ __device__ __forceinline__ void pair_wave_a(PairShared& sh, const RolloutArgs& A
             salp::load_cold<false>(C, a.S, a.P, i);
             Hot hb;
             salp::unspill<false>(hb, sl, a.P, env_id);
-            rollout_boundary<false, POL>(hb, &C, a.P, i, env_id, pending, active, steps, a.max_steps, a.B,
-                                         a.reward_sum, a.R, salp::Cache32{sh.cache32 + s, kPairEnvs});
+            if (POL)
+                rollout_boundary<false, POL>(hb, &C, a.P, i, env_id, pending, active, steps, a.max_steps, a.B,
+                                             a.reward_sum, a.R, salp::Cache32{sh.cache32 + s, kPairEnvs},
+                                             ValuesToPartner{jobs, grp, s, 0});
+            else
+                rollout_boundary<false, POL>(hb, &C, a.P, i, env_id, pending, active, steps, a.max_steps, a.B,
+                                             a.reward_sum, a.R, salp::Cache32{sh.cache32 + s, kPairEnvs});
             salp::store_cold<false>(C, a.S, a.P, i);
             salp::spill<false>(hb, sl);
         }
+        if (POL) pair_publish(&jobs->done[grp], (int)c + 1);   // this boundary's jobs are all out
         if (last) {
             const RolloutArgs a = fresh_args();
             Hot h;
@@ -1042,7 +1160,8 @@ __device__ __forceinline__ void pair_wave_a(PairShared& sh, const RolloutArgs& A
     }
 }
 
-__device__ __forceinline__ void pair_wave_b(PairShared& sh, const RolloutArgs& A, int grp, int lane) {
+template <bool POL>
+__device__ __forceinline__ void pair_wave_b(PairShared& sh, PairJobs* jobs, const RolloutArgs& A, int grp, int lane) {
     const Params& P = A.P;
     const int seat = grp * 64 + lane;
     int s = seat;
@@ -1060,8 +1179,10 @@ __device__ __forceinline__ void pair_wave_b(PairShared& sh, const RolloutArgs& A
     bool all_done = false;
     PairProf prof;
     prof.start();
+    int taken = 0;   // POL: job buffers evaluated
     for (int64_t c = 0;; ++c) {
         const bool last = c == A.n_chunks || all_done;
+        if (POL) pair_value_jobs(*jobs, A, grp, s, c, taken);   // while the A wave runs this boundary
         if (last) {
             prof.lap(PP_BOUNDARY);
             prof.flush(1);
@@ -1126,13 +1247,23 @@ __device__ __forceinline__ void pair_wave_b(PairShared& sh, const RolloutArgs& A
     }
 }
 
+// The job buffers exist (LDS) in the salp_collect instance only.
+template <bool POL>
+__device__ __forceinline__ PairJobs* pair_jobs_lds() {
+    __shared__ PairJobs j;
+    return &j;
+}
+template <>
+__device__ __forceinline__ PairJobs* pair_jobs_lds<false>() { return nullptr; }
+
 template <bool POL>
 __global__ __launch_bounds__(kBlock) void k_rollout_pair(RolloutArgs A) {
     __shared__ PairShared sh;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = (int)(threadIdx.x & 63);
-    if (wave & 1) pair_wave_b(sh, A, wave >> 1, lane);
-    else pair_wave_a<POL>(sh, A, wave >> 1, lane);
+    PairJobs* const jobs = pair_jobs_lds<POL>();
+    if (wave & 1) pair_wave_b<POL>(sh, jobs, A, wave >> 1, lane);
+    else pair_wave_a<POL>(sh, jobs, A, wave >> 1, lane);
 }
 
 // The ABI's field-major state (state[f * n + i]) <-> the handle's layout
