@@ -868,6 +868,27 @@ __device__ __forceinline__ void pair_publish(int* flag, int value) {
     __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// SALP_PAIR_FASTSYNC=1: the packet protocol on LDS's in-order execution of a
+// wave's DS instructions instead of release / acquire: the writer stores the
+// data and then the counter as volatile LDS stores (program order, no wait
+// for the data stores to land), the reader loads the counter and the data in
+// one round (the counter load executes first) and keeps the data once the
+// counter shows the packet.  One LDS round trip per receive instead of two,
+// no store-completion wait per publish.
+#ifndef SALP_PAIR_FASTSYNC
+#define SALP_PAIR_FASTSYNC 0
+#endif
+template <class F>
+__device__ __forceinline__ bool pair_wait_read(int* flag, int target, F read) {
+    for (int it = 0; it < kPairSpin; ++it) {
+        const int f = __builtin_amdgcn_readfirstlane(*(volatile int*)flag);
+        read();
+        if (f >= target) return true;
+    }
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_pair_timeouts, 1u);
+    return false;
+}
+
 struct ValuesToPartner {
     static constexpr bool kDefer = true;
     PairJobs* J;
@@ -1105,20 +1126,37 @@ __device__ __forceinline__ void pair_wave_a(PairShared& sh, PairJobs* jobs, cons
             const auto publish = [&](int mode) {
                 double X[3], jt[2];
                 salp::a_prepare(h, PV, X, jt);
-                double* const o = ab + (pub & 1) * kXchAB * 64;
-                o[0 * 64] = X[0]; o[1 * 64] = X[1]; o[2 * 64] = X[2]; o[3 * 64] = jt[0]; o[4 * 64] = jt[1];
-                if (lane == 0) sh.mode[grp][pub & 1] = mode;
-                pair_publish(&sh.cnt[grp][0], ++pub);
+                if (SALP_PAIR_FASTSYNC) {
+                    volatile double* const o = ab + (pub & 1) * kXchAB * 64;
+                    o[0 * 64] = X[0]; o[1 * 64] = X[1]; o[2 * 64] = X[2]; o[3 * 64] = jt[0]; o[4 * 64] = jt[1];
+                    ((volatile int*)sh.mode[grp])[pub & 1] = mode;
+                    *(volatile int*)&sh.cnt[grp][0] = ++pub;
+                } else {
+                    double* const o = ab + (pub & 1) * kXchAB * 64;
+                    o[0 * 64] = X[0]; o[1 * 64] = X[1]; o[2 * 64] = X[2]; o[3 * 64] = jt[0]; o[4 * 64] = jt[1];
+                    if (lane == 0) sh.mode[grp][pub & 1] = mode;
+                    pair_publish(&sh.cnt[grp][0], ++pub);
+                }
             };
             bool ok = true;
             const auto recv = [&]() {
                 prof.lap(PP_PUBLISH);
-                ok = pair_wait(&sh.cnt[grp][1], rcv + 1) && ok;
-                prof.lap(PP_WAIT);
-                const double* const q = ba + (rcv & 1) * kXchBA * 64;
-                h.w0 = q[0 * 64]; h.w1 = q[1 * 64]; h.w2 = q[2 * 64]; h.al1 = q[3 * 64]; h.al2 = q[4 * 64];
-                h.sp = q[5 * 64]; h.cp = q[6 * 64]; h.st = q[7 * 64]; h.cth = q[8 * 64]; h.ss = q[9 * 64];
-                h.cs = q[10 * 64]; h.kc0 = q[11 * 64]; h.kc1 = q[12 * 64];
+                if (SALP_PAIR_FASTSYNC) {
+                    volatile const double* const q = ba + (rcv & 1) * kXchBA * 64;
+                    ok = pair_wait_read(&sh.cnt[grp][1], rcv + 1, [&] {
+                        h.w0 = q[0 * 64]; h.w1 = q[1 * 64]; h.w2 = q[2 * 64]; h.al1 = q[3 * 64]; h.al2 = q[4 * 64];
+                        h.sp = q[5 * 64]; h.cp = q[6 * 64]; h.st = q[7 * 64]; h.cth = q[8 * 64]; h.ss = q[9 * 64];
+                        h.cs = q[10 * 64]; h.kc0 = q[11 * 64]; h.kc1 = q[12 * 64];
+                    }) && ok;
+                    prof.lap(PP_WAIT);
+                } else {
+                    ok = pair_wait(&sh.cnt[grp][1], rcv + 1) && ok;
+                    prof.lap(PP_WAIT);
+                    const double* const q = ba + (rcv & 1) * kXchBA * 64;
+                    h.w0 = q[0 * 64]; h.w1 = q[1 * 64]; h.w2 = q[2 * 64]; h.al1 = q[3 * 64]; h.al2 = q[4 * 64];
+                    h.sp = q[5 * 64]; h.cp = q[6 * 64]; h.st = q[7 * 64]; h.cth = q[8 * 64]; h.ss = q[9 * 64];
+                    h.cs = q[10 * 64]; h.kc0 = q[11 * 64]; h.kc1 = q[12 * 64];
+                }
                 ++rcv;
                 prof.lap(PP_READ);
             };
@@ -1207,11 +1245,19 @@ __device__ __forceinline__ void pair_wave_b(PairShared& sh, PairJobs* jobs, cons
             double* const ab = sh.big + grp * 2 * kXchAB * 64 + lane;
             double* const ba = sh.big + kXchBase + grp * 2 * kXchBA * 64 + lane;
             const auto publish = [&]() {
-                double* const o = ba + (pub & 1) * kXchBA * 64;
-                o[0 * 64] = h.w0; o[1 * 64] = h.w1; o[2 * 64] = h.w2; o[3 * 64] = h.al1; o[4 * 64] = h.al2;
-                o[5 * 64] = h.sp; o[6 * 64] = h.cp; o[7 * 64] = h.st; o[8 * 64] = h.cth; o[9 * 64] = h.ss;
-                o[10 * 64] = h.cs; o[11 * 64] = h.kc0; o[12 * 64] = h.kc1;
-                pair_publish(&sh.cnt[grp][1], ++pub);
+                if (SALP_PAIR_FASTSYNC) {
+                    volatile double* const o = ba + (pub & 1) * kXchBA * 64;
+                    o[0 * 64] = h.w0; o[1 * 64] = h.w1; o[2 * 64] = h.w2; o[3 * 64] = h.al1; o[4 * 64] = h.al2;
+                    o[5 * 64] = h.sp; o[6 * 64] = h.cp; o[7 * 64] = h.st; o[8 * 64] = h.cth; o[9 * 64] = h.ss;
+                    o[10 * 64] = h.cs; o[11 * 64] = h.kc0; o[12 * 64] = h.kc1;
+                    *(volatile int*)&sh.cnt[grp][1] = ++pub;
+                } else {
+                    double* const o = ba + (pub & 1) * kXchBA * 64;
+                    o[0 * 64] = h.w0; o[1 * 64] = h.w1; o[2 * 64] = h.w2; o[3 * 64] = h.al1; o[4 * 64] = h.al2;
+                    o[5 * 64] = h.sp; o[6 * 64] = h.cp; o[7 * 64] = h.st; o[8 * 64] = h.cth; o[9 * 64] = h.ss;
+                    o[10 * 64] = h.cs; o[11 * 64] = h.kc0; o[12 * 64] = h.kc1;
+                    pair_publish(&sh.cnt[grp][1], ++pub);
+                }
             };
             // a bound on the ticks of one chunk (A ends it earlier)
             const int64_t cap = 4 + (int64_t)A.chunk + (((int64_t)A.chunk * A.steady_q8) >> 8);
@@ -1219,11 +1265,25 @@ __device__ __forceinline__ void pair_wave_b(PairShared& sh, PairJobs* jobs, cons
             publish();
             prof.lap(PP_PUBLISH);
             for (int64_t it = 0; it < cap; ++it) {
-                const bool ok = pair_wait(&sh.cnt[grp][0], rcv + 1);
-                prof.lap(PP_WAIT);
-                const double* const q = ab + (rcv & 1) * kXchAB * 64;
-                h.X0 = q[0 * 64]; h.X1 = q[1 * 64]; h.X2 = q[2 * 64]; h.jt1 = q[3 * 64]; h.jt2 = q[4 * 64];
-                const int mode = __builtin_amdgcn_readfirstlane(sh.mode[grp][rcv & 1]);
+                bool ok;
+                int mode;
+                if (SALP_PAIR_FASTSYNC) {
+                    volatile const double* const q = ab + (rcv & 1) * kXchAB * 64;
+                    volatile const int* const qm = &sh.mode[grp][rcv & 1];
+                    int mv = 0;
+                    ok = pair_wait_read(&sh.cnt[grp][0], rcv + 1, [&] {
+                        h.X0 = q[0 * 64]; h.X1 = q[1 * 64]; h.X2 = q[2 * 64]; h.jt1 = q[3 * 64]; h.jt2 = q[4 * 64];
+                        mv = *qm;
+                    });
+                    mode = __builtin_amdgcn_readfirstlane(mv);
+                    prof.lap(PP_WAIT);
+                } else {
+                    ok = pair_wait(&sh.cnt[grp][0], rcv + 1);
+                    prof.lap(PP_WAIT);
+                    const double* const q = ab + (rcv & 1) * kXchAB * 64;
+                    h.X0 = q[0 * 64]; h.X1 = q[1 * 64]; h.X2 = q[2 * 64]; h.jt1 = q[3 * 64]; h.jt2 = q[4 * 64];
+                    mode = __builtin_amdgcn_readfirstlane(sh.mode[grp][rcv & 1]);
+                }
                 ++rcv;
                 prof.lap(PP_READ);
                 if (mode == salp::PM_END || !ok) break;
@@ -1445,14 +1505,14 @@ int32_t rollout_steady_q8() {
     return q;
 }
 // The same budget for k_rollout_pair, whose steady ticks cost relatively more
-// (the per-tick packet exchange is the same for every kind of tick): q = 380
-// (32 768 envs, profiles/r4_experiments.md r4h: 300 / 380 / 480 x chunk
+// (the per-tick packet exchange is the same for every kind of tick): q = 320
+// (32 768 envs, profiles/r4_experiments.md r4h / r4q: 300-480 x chunk
 // 256 / 384 / 512).  SALP_PAIR_STEADY_Q8 overrides it.
 int32_t pair_steady_q8() {
     static const int32_t q = [] {
         const char* e = std::getenv("SALP_PAIR_STEADY_Q8");
         const long v = e ? std::strtol(e, nullptr, 10) : 0;
-        return (int32_t)(v > 0 && v < (1 << 16) ? v : 380);
+        return (int32_t)(v > 0 && v < (1 << 16) ? v : 320);
     }();
     return q;
 }
