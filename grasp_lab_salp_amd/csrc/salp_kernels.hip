@@ -878,6 +878,15 @@ __device__ __forceinline__ void pair_publish(int* flag, int value) {
 #ifndef SALP_PAIR_FASTSYNC
 #define SALP_PAIR_FASTSYNC 0
 #endif
+// SALP_PAIR_PREFETCH=1: a full tick's clock / phase / geometry (salp_pair.h
+// pre_a, pre_b: no partner data) computed between publishing a packet and
+// waiting for the partner's, so that it fills the wait; wave B computes it
+// speculatively after a full tick (the next is full too until the chunk's full
+// ticks end).
+#ifndef SALP_PAIR_PREFETCH
+#define SALP_PAIR_PREFETCH 0
+#endif
+
 template <class F>
 __device__ __forceinline__ bool pair_wait_read(int* flag, int target, F read) {
     for (int it = 0; it < kPairSpin; ++it) {
@@ -1163,6 +1172,8 @@ __device__ __forceinline__ void pair_wave_a(PairShared& sh, PairJobs* jobs, cons
             prof.lap(PP_BOUNDARY);
             int mode = decide();
             publish(mode);
+            salp::PreA pre{};
+            if (SALP_PAIR_PREFETCH && mode == salp::PM_FULL) pre = salp::pre_a<salp::PM_FULL>(h, PV, c32);
             recv();
             // pend: the lane's last tick still owes its world-frame position
             // update (step_a does it at the start of the next tick, with the
@@ -1171,7 +1182,9 @@ __device__ __forceinline__ void pair_wave_a(PairShared& sh, PairJobs* jobs, cons
             while (mode != salp::PM_END && ok) {
                 const bool ticks = h.ct < h.b2;
                 if (mode == salp::PM_FULL) {
-                    if (ticks) salp::step_a<salp::PM_FULL>(h, PV, c32, pend);
+                    if (ticks)
+                        salp::step_a<salp::PM_FULL>(h, PV, SALP_PAIR_PREFETCH ? pre : salp::pre_a<salp::PM_FULL>(h, PV, c32),
+                                                    pend);
                 } else if (mode == salp::PM_STEADY) {
                     bool settled = true;
                     if (ticks) settled = salp::step_a<salp::PM_STEADY>(h, PV, c32, pend);
@@ -1183,6 +1196,7 @@ __device__ __forceinline__ void pair_wave_a(PairShared& sh, PairJobs* jobs, cons
                 mode = decide();
                 prof.lap(PP_TICK);
                 publish(mode);
+                if (SALP_PAIR_PREFETCH && mode == salp::PM_FULL) pre = salp::pre_a<salp::PM_FULL>(h, PV, c32);
                 recv();
             }
             if (pend) salp::a_world(h, PV);
@@ -1264,6 +1278,8 @@ __device__ __forceinline__ void pair_wave_b(PairShared& sh, PairJobs* jobs, cons
             prof.lap(PP_BOUNDARY);
             publish();
             prof.lap(PP_PUBLISH);
+            bool prefetched = false;
+            salp::PreB pre{};
             for (int64_t it = 0; it < cap; ++it) {
                 bool ok;
                 int mode;
@@ -1288,13 +1304,16 @@ __device__ __forceinline__ void pair_wave_b(PairShared& sh, PairJobs* jobs, cons
                 prof.lap(PP_READ);
                 if (mode == salp::PM_END || !ok) break;
                 if (h.ct < h.b2) {
-                    if (mode == salp::PM_FULL) salp::step_b<salp::PM_FULL>(h, PV, c32);
+                    if (mode == salp::PM_FULL)
+                        salp::step_b<salp::PM_FULL>(h, PV, prefetched ? pre : salp::pre_b<salp::PM_FULL>(h, PV, c32));
                     else if (mode == salp::PM_STEADY) salp::step_b<salp::PM_STEADY>(h, PV, c32);
                     else salp::step_b<salp::PM_SETTLED>(h, PV, c32);
                 }
                 prof.lap(PP_TICK);
                 publish();
                 prof.lap(PP_PUBLISH);
+                prefetched = SALP_PAIR_PREFETCH && mode == salp::PM_FULL;
+                if (prefetched) pre = salp::pre_b<salp::PM_FULL>(h, PV, c32);   // the next tick, if full
             }
         }
         prof.lap(PP_BOUNDARY);

@@ -125,21 +125,17 @@ SD void a_world(HotA& h, const Params&) {
  * straight path when every ticking lane's angles are small, then the yaw's
  * for wave A.  Every value is the expression tick() computes. */
 
-/* The world-frame update owed for the previous tick (pend: it ticked), then
- * this tick.  Returns, for a steady tick, whether the lane is settled. */
+/* A tick's clock, phase and (full ticks) mass-side geometry: a function of
+ * wave A's own state alone, so it can be computed before the partner's
+ * packet arrives (SALP_PAIR_PREFETCH). */
+struct PreA {
+    double ct, L, W, V, com, comr, coma, m, mr, speed, rm;
+    int phase;
+    bool f;
+};
 template <int MODE>
-SD bool step_a(HotA& h, const Params& P, Cache32 c32, bool pend) {
-    constexpr bool STEADY = MODE != PM_FULL, SETTLED = MODE == PM_SETTLED;
-    {   /* a_world of the previous tick, with v before this tick's Newton */
-        const Rot R = rot_sc(h.sp, h.cp, h.st, h.cth, h.ss, h.cs);
-        double vw[3];
-        rot_apply(R, h.v0, h.v1, h.v2, vw);
-        const double p0 = sm_mad(vw[0], DT, h.p0), p1 = sm_mad(vw[1], DT, h.p1), p2 = sm_mad(vw[2], DT, h.p2);
-        h.p0 = pend ? p0 : h.p0;
-        h.p1 = pend ? p1 : h.p1;
-        h.p2 = pend ? p2 : h.p2;
-    }
-    /* clock, phase and (full ticks) the mass-side geometry of this tick */
+SD PreA pre_a(const HotA& h, const Params& P, Cache32 c32) {
+    constexpr bool STEADY = MODE != PM_FULL;
     double ct = h.ct;
     int phase = h.phase;
     pair_clock<STEADY>(ct, phase, h.b1, h.b2, h.mx);
@@ -164,6 +160,24 @@ SD bool step_a(HotA& h, const Params& P, Cache32 c32, bool pend) {
         mr = ng.mr;
         sp = ng.speed;
         rmn = rcp_of(mn).r;
+    }
+    return PreA{ct, L, W, V, com, comr, coma, mn, mr, sp, rmn, phase, f};
+}
+
+/* The world-frame update owed for the previous tick (pend: it ticked), then
+ * this tick with its clock / geometry g (pre_a).  Returns, for a steady tick,
+ * whether the lane is settled. */
+template <int MODE>
+SD bool step_a(HotA& h, const Params& P, const PreA& g, bool pend) {
+    constexpr bool STEADY = MODE != PM_FULL, SETTLED = MODE == PM_SETTLED;
+    {   /* a_world of the previous tick, with v before this tick's Newton */
+        const Rot R = rot_sc(h.sp, h.cp, h.st, h.cth, h.ss, h.cs);
+        double vw[3];
+        rot_apply(R, h.v0, h.v1, h.v2, vw);
+        const double p0 = sm_mad(vw[0], DT, h.p0), p1 = sm_mad(vw[1], DT, h.p1), p2 = sm_mad(vw[2], DT, h.p2);
+        h.p0 = pend ? p0 : h.p0;
+        h.p1 = pend ? p1 : h.p1;
+        h.p2 = pend ? p2 : h.p2;
     }
     /* Newton's equations with the tick-start values */
     const double m = h.m;
@@ -192,8 +206,8 @@ SD bool step_a(HotA& h, const Params& P, Cache32 c32, bool pend) {
     h.v0 = sm_mad(na0, DT, h.v0); h.v1 = sm_mad(na1, DT, h.v1); h.v2 = sm_mad(na2, DT, h.v2);
     h.q0 = sm_mad(h.v0, DT, h.q0); h.q1 = sm_mad(h.v1, DT, h.q1); h.q2 = sm_mad(h.v2, DT, h.q2);
     /* commit the tick's clock and properties */
-    h.ct = ct;
-    h.phase = phase;
+    h.ct = g.ct;
+    h.phase = g.phase;
     h.time += DT;
     h.pV = h.V;
     if (STEADY) {
@@ -214,16 +228,26 @@ SD bool step_a(HotA& h, const Params& P, Cache32 c32, bool pend) {
         return zero();
     }
     h.pv32 = h.g32;
-    h.L = L; h.W = W; h.g32 = f;
-    h.V = V; h.com = com; h.comr = comr; h.coma = coma;
-    h.m = mn; h.mr = mr; h.speed = sp; h.rm = rmn;
+    h.L = g.L; h.W = g.W; h.g32 = g.f;
+    h.V = g.V; h.com = g.com; h.comr = g.comr; h.coma = g.coma;
+    h.m = g.m; h.mr = g.mr; h.speed = g.speed; h.rm = g.rm;
     return false;
 }
-
 template <int MODE>
-SD void step_b(HotB& h, const Params& P, Cache32 c32) {
-    constexpr bool STEADY = MODE != PM_FULL, SETTLED = MODE == PM_SETTLED;
-    /* clock, phase and (full ticks) the shape-side geometry of this tick */
+SD bool step_a(HotA& h, const Params& P, Cache32 c32, bool pend) {
+    return step_a<MODE>(h, P, pre_a<MODE>(h, P, c32), pend);
+}
+
+/* Wave B's clock, phase and (full ticks) shape-side geometry of a tick. */
+struct PreB {
+    double ct, L, W;
+    Geo ng;
+    int phase;
+    bool f;
+};
+template <int MODE>
+SD PreB pre_b(const HotB& h, const Params& P, Cache32 c32) {
+    constexpr bool STEADY = MODE != PM_FULL;
     double ct = h.ct;
     int phase = h.phase;
     pair_clock<STEADY>(ct, phase, h.b1, h.b2, h.mx);
@@ -242,6 +266,12 @@ SD void step_b(HotB& h, const Params& P, Cache32 c32) {
         ng.rI0 = rcp_of(ng.I0).r;
         ng.rI1 = rcp_of(ng.I1).r;
     }
+    return PreB{ct, L, W, ng, phase, f};
+}
+
+template <int MODE>
+SD void step_b(HotB& h, const Params& P, const PreB& g) {
+    constexpr bool STEADY = MODE != PM_FULL, SETTLED = MODE == PM_SETTLED;
     /* Euler's equations with the tick-start values */
     const double I0 = h.I0, I1 = h.I1;
     double iw0 = I0 * h.w0, iw1 = I1 * h.w1, iw2 = I1 * h.w2;
@@ -279,16 +309,20 @@ SD void step_b(HotB& h, const Params& P, Cache32 c32) {
         h.e0 = sm_mad(r0, DT, h.e0); h.e1 = sm_mad(r1, DT, h.e1); h.e2 = sm_mad(r2, DT, h.e2);
     }
     h.g0 = sm_mad(h.w0, DT, h.g0); h.g1 = sm_mad(h.w1, DT, h.g1); h.g2 = sm_mad(h.w2, DT, h.g2);
-    h.ct = ct;
-    h.phase = phase;
+    h.ct = g.ct;
+    h.phase = g.phase;
     if (!STEADY) {
-        h.L = L; h.W = W; h.g32 = f;
-        h.I0 = ng.I0; h.I1 = ng.I1; h.rI0 = ng.rI0; h.rI1 = ng.rI1;
-        h.kc0 = ng.kc0; h.kc1 = ng.kc1; h.ra0 = ng.ra0; h.ra1 = ng.ra1;
-        h.dimx = ng.dimx; h.dimy = ng.dimy;
+        h.L = g.L; h.W = g.W; h.g32 = g.f;
+        h.I0 = g.ng.I0; h.I1 = g.ng.I1; h.rI0 = g.ng.rI0; h.rI1 = g.ng.rI1;
+        h.kc0 = g.ng.kc0; h.kc1 = g.ng.kc1; h.ra0 = g.ng.ra0; h.ra1 = g.ng.ra1;
+        h.dimx = g.ng.dimx; h.dimy = g.ng.dimy;
     }
     sincos2_p(h.e0, h.e1, &h.sp, &h.cp, &h.st, &h.cth, P.sk);
     sm_sincos_nb_p(h.e2, &h.ss, &h.cs, P.sk);   /* yaw: wave A's world-frame update */
+}
+template <int MODE>
+SD void step_b(HotB& h, const Params& P, Cache32 c32) {
+    step_b<MODE>(h, P, pre_b<MODE>(h, P, c32));
 }
 
 /* ---------------------------------------- LDS slot <-> the two waves */
