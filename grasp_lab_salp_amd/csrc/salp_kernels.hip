@@ -834,7 +834,7 @@ struct PairShared {
     int64_t steps[kPairEnvs];
     int16_t slot[2][kPairEnvs];
     uint64_t mask[2][2], amask[2][2];
-    int cnt[2][2];                            // [group][role]: packets published
+    int cnt[2][3];                            // [group][A, B (SALP_PAIR_SPLIT: B's first), B's second]: packets published
     int mode[2][2];                           // [group][buffer]: the tick kind wave A sent
     uint8_t flags[kPairEnvs];
 };
@@ -896,6 +896,39 @@ __device__ __forceinline__ bool pair_wait_read(int* flag, int target, F read) {
     }
     if ((threadIdx.x & 63) == 0) atomicAdd(&g_pair_timeouts, 1u);
     return false;
+}
+
+// SALP_PAIR_SPLIT=1: wave B sends two packets per tick instead of one.  The
+// first (new angular velocity, angular accelerations y, z) right after Euler's
+// equations, which is all wave A's next Newton step needs; the second (roll /
+// pitch sin/cos at the new angles, the new yaw, the drag-force coefficients)
+// after the angle integration, sin/cos and geometry, which wave A needs only
+// for the world-frame update of the tick just done (now after its next packet
+// went out) and its next Newton step.  Wave A computes the yaw's sin/cos
+// itself (its share of the tick was the lighter one).  The two waves' critical
+// loop is then Newton <-> Euler; the rest of each half overlaps the partner.
+#ifndef SALP_PAIR_SPLIT
+#define SALP_PAIR_SPLIT 0
+#endif
+// A packet out / in, with either protocol (SALP_PAIR_FASTSYNC or
+// release / acquire).  write(o) / read(q) store / load the packet's doubles
+// through o / q (volatile pointers under FASTSYNC).
+template <class W>
+__device__ __forceinline__ void xch_put(double* o, int* cnt, int value, W write) {
+    if (SALP_PAIR_FASTSYNC) {
+        write((volatile double*)o);
+        *(volatile int*)cnt = value;
+    } else {
+        write(o);
+        pair_publish(cnt, value);
+    }
+}
+template <class R>
+__device__ __forceinline__ bool xch_get(const double* q, int* cnt, int target, R read) {
+    if (SALP_PAIR_FASTSYNC) return pair_wait_read(cnt, target, [&] { read((volatile const double*)q); });
+    const bool ok = pair_wait(cnt, target);
+    read(q);
+    return ok;
 }
 
 struct ValuesToPartner {
@@ -1034,7 +1067,7 @@ __device__ __forceinline__ void pair_wave_a(PairShared& sh, PairJobs* jobs, cons
             salp::fill_cache32(P, h.c, salp::Cache32{sh.cache32 + s, kPairEnvs});
         }
         salp::spill<false>(h, salp::SpillSlot{sh.big + s, kPairEnvs});
-        if (lane < 2) sh.cnt[grp][lane] = 0;
+        if (lane < 3) sh.cnt[grp][lane] = 0;
         if (POL && lane == 0) {
             jobs->cnt[grp] = 0;
             jobs->done[grp] = 0;
@@ -1171,6 +1204,57 @@ __device__ __forceinline__ void pair_wave_a(PairShared& sh, PairJobs* jobs, cons
             };
             prof.lap(PP_BOUNDARY);
             int mode = decide();
+            if (SALP_PAIR_SPLIT) {
+                double* const b1p = ba;                 // wave B's first packets: 2 x 5 doubles
+                double* const b2p = ba + 2 * 5 * 64;    // its second packets: 2 x 7 doubles
+                const auto put = [&](int md) {
+                    double X[3], jt[2];
+                    salp::a_prepare(h, PV, X, jt);
+                    const int b = pub & 1;
+                    xch_put(ab + b * kXchAB * 64, &sh.cnt[grp][0], pub + 1, [&](auto o) {
+                        o[0 * 64] = X[0]; o[1 * 64] = X[1]; o[2 * 64] = X[2]; o[3 * 64] = jt[0]; o[4 * 64] = jt[1];
+                        if (lane == 0) ((volatile int*)sh.mode[grp])[b] = md;
+                    });
+                    ++pub;
+                };
+                put(mode);
+                int rcv2 = rcv;   // B's second packets so far: one per tick, like its first
+                while (mode != salp::PM_END && ok) {
+                    const bool ticks = h.ct < h.b2;
+                    if (mode == salp::PM_FULL) {
+                        if (ticks) salp::step_a_newton<salp::PM_FULL>(h, PV, salp::pre_a<salp::PM_FULL>(h, PV, c32));
+                    } else if (mode == salp::PM_STEADY) {
+                        bool settled = true;
+                        if (ticks)
+                            settled = salp::step_a_newton<salp::PM_STEADY>(h, PV,
+                                                                           salp::pre_a<salp::PM_STEADY>(h, PV, c32));
+                        if (__all(settled)) stage = 2;
+                    } else {
+                        if (ticks)
+                            salp::step_a_newton<salp::PM_SETTLED>(h, PV, salp::pre_a<salp::PM_SETTLED>(h, PV, c32));
+                    }
+                    mode = decide();
+                    prof.lap(PP_TICK);
+                    put(mode);
+                    prof.lap(PP_PUBLISH);
+                    double yaw = 0.0;
+                    ok = xch_get(b2p + (rcv2 & 1) * 7 * 64, &sh.cnt[grp][2], rcv2 + 1, [&](auto q) {
+                        h.sp = q[0 * 64]; h.cp = q[1 * 64]; h.st = q[2 * 64]; h.cth = q[3 * 64]; yaw = q[4 * 64];
+                        h.kc0 = q[5 * 64]; h.kc1 = q[6 * 64];
+                    }) && ok;
+                    ++rcv2;
+                    prof.lap(PP_WAIT);
+                    if (ticks) salp::a_world_yaw(h, PV, yaw);
+                    prof.lap(PP_WORLD);
+                    if (mode != salp::PM_END)
+                        ok = xch_get(b1p + (rcv & 1) * 5 * 64, &sh.cnt[grp][1], rcv + 1, [&](auto q) {
+                            h.w0 = q[0 * 64]; h.w1 = q[1 * 64]; h.w2 = q[2 * 64]; h.al1 = q[3 * 64]; h.al2 = q[4 * 64];
+                        }) && ok;
+                    ++rcv;   // counted at the end of the chunk too: wave B sent that packet
+                    prof.lap(PP_WAIT);
+                }
+                rcv = rcv2;
+            } else {
             publish(mode);
             salp::PreA pre{};
             if (SALP_PAIR_PREFETCH && mode == salp::PM_FULL) pre = salp::pre_a<salp::PM_FULL>(h, PV, c32);
@@ -1201,6 +1285,7 @@ __device__ __forceinline__ void pair_wave_a(PairShared& sh, PairJobs* jobs, cons
             }
             if (pend) salp::a_world(h, PV);
             prof.lap(PP_WORLD);
+            }
         }
         prof.lap(PP_BOUNDARY);
         __syncthreads();   // #3: packets done
@@ -1276,6 +1361,48 @@ __device__ __forceinline__ void pair_wave_b(PairShared& sh, PairJobs* jobs, cons
             // a bound on the ticks of one chunk (A ends it earlier)
             const int64_t cap = 4 + (int64_t)A.chunk + (((int64_t)A.chunk * A.steady_q8) >> 8);
             prof.lap(PP_BOUNDARY);
+            if (SALP_PAIR_SPLIT) {
+                double* const b1p = ba;
+                double* const b2p = ba + 2 * 5 * 64;
+                for (int64_t it = 0; it < cap; ++it) {
+                    int mv = 0;
+                    const int b = rcv & 1;
+                    const bool ok = xch_get(ab + b * kXchAB * 64, &sh.cnt[grp][0], rcv + 1, [&](auto q) {
+                        h.X0 = q[0 * 64]; h.X1 = q[1 * 64]; h.X2 = q[2 * 64]; h.jt1 = q[3 * 64]; h.jt2 = q[4 * 64];
+                        mv = ((volatile const int*)sh.mode[grp])[b];
+                    });
+                    const int mode = __builtin_amdgcn_readfirstlane(mv);
+                    ++rcv;
+                    prof.lap(PP_WAIT);
+                    if (mode == salp::PM_END || !ok) break;
+                    const bool ticks = h.ct < h.b2;
+                    if (ticks) {
+                        if (mode == salp::PM_FULL) salp::step_b1<salp::PM_FULL>(h, PV);
+                        else if (mode == salp::PM_STEADY) salp::step_b1<salp::PM_STEADY>(h, PV);
+                        else salp::step_b1<salp::PM_SETTLED>(h, PV);
+                    }
+                    prof.lap(PP_TICK);
+                    xch_put(b1p + (pub & 1) * 5 * 64, &sh.cnt[grp][1], pub + 1, [&](auto o) {
+                        o[0 * 64] = h.w0; o[1 * 64] = h.w1; o[2 * 64] = h.w2; o[3 * 64] = h.al1; o[4 * 64] = h.al2;
+                    });
+                    prof.lap(PP_PUBLISH);
+                    if (ticks) {
+                        if (mode == salp::PM_FULL)
+                            salp::step_b2<salp::PM_FULL, false>(h, PV, salp::pre_b<salp::PM_FULL>(h, PV, c32));
+                        else if (mode == salp::PM_STEADY)
+                            salp::step_b2<salp::PM_STEADY, false>(h, PV, salp::pre_b<salp::PM_STEADY>(h, PV, c32));
+                        else
+                            salp::step_b2<salp::PM_SETTLED, false>(h, PV, salp::pre_b<salp::PM_SETTLED>(h, PV, c32));
+                    }
+                    prof.lap(PP_TICK);
+                    xch_put(b2p + (pub & 1) * 7 * 64, &sh.cnt[grp][2], pub + 1, [&](auto o) {
+                        o[0 * 64] = h.sp; o[1 * 64] = h.cp; o[2 * 64] = h.st; o[3 * 64] = h.cth; o[4 * 64] = h.e2;
+                        o[5 * 64] = h.kc0; o[6 * 64] = h.kc1;
+                    });
+                    ++pub;
+                    prof.lap(PP_PUBLISH);
+                }
+            } else {
             publish();
             prof.lap(PP_PUBLISH);
             bool prefetched = false;
@@ -1314,6 +1441,7 @@ __device__ __forceinline__ void pair_wave_b(PairShared& sh, PairJobs* jobs, cons
                 prof.lap(PP_PUBLISH);
                 prefetched = SALP_PAIR_PREFETCH && mode == salp::PM_FULL;
                 if (prefetched) pre = salp::pre_b<salp::PM_FULL>(h, PV, c32);   // the next tick, if full
+            }
             }
         }
         prof.lap(PP_BOUNDARY);

@@ -168,8 +168,9 @@ SD PreA pre_a(const HotA& h, const Params& P, Cache32 c32) {
  * this tick with its clock / geometry g (pre_a).  Returns, for a steady tick,
  * whether the lane is settled. */
 template <int MODE>
+SD bool step_a_newton(HotA& h, const Params& P, const PreA& g);
+template <int MODE>
 SD bool step_a(HotA& h, const Params& P, const PreA& g, bool pend) {
-    constexpr bool STEADY = MODE != PM_FULL, SETTLED = MODE == PM_SETTLED;
     {   /* a_world of the previous tick, with v before this tick's Newton */
         const Rot R = rot_sc(h.sp, h.cp, h.st, h.cth, h.ss, h.cs);
         double vw[3];
@@ -179,7 +180,13 @@ SD bool step_a(HotA& h, const Params& P, const PreA& g, bool pend) {
         h.p1 = pend ? p1 : h.p1;
         h.p2 = pend ? p2 : h.p2;
     }
-    /* Newton's equations with the tick-start values */
+    return step_a_newton<MODE>(h, P, g);
+}
+/* Newton's equations with the tick-start values, then the tick's clock and
+ * mass-side properties committed. */
+template <int MODE>
+SD bool step_a_newton(HotA& h, const Params& P, const PreA& g) {
+    constexpr bool STEADY = MODE != PM_FULL, SETTLED = MODE == PM_SETTLED;
     const double m = h.m;
     double mv0 = m * h.v0, mv1 = m * h.v1, mv2 = m * h.v2;
     double cf0 = -cross_c(h.w1, mv2, h.w2, mv1), cf1 = -cross_c(h.w2, mv0, h.w0, mv2),
@@ -269,10 +276,11 @@ SD PreB pre_b(const HotB& h, const Params& P, Cache32 c32) {
     return PreB{ct, L, W, ng, phase, f};
 }
 
+/* Euler's equations with the tick-start values: the new angular velocity and
+ * acceleration (all wave A needs before its next Newton step). */
 template <int MODE>
-SD void step_b(HotB& h, const Params& P, const PreB& g) {
-    constexpr bool STEADY = MODE != PM_FULL, SETTLED = MODE == PM_SETTLED;
-    /* Euler's equations with the tick-start values */
+SD void step_b1(HotB& h, const Params& P) {
+    constexpr bool SETTLED = MODE == PM_SETTLED;
     const double I0 = h.I0, I1 = h.I1;
     double iw0 = I0 * h.w0, iw1 = I1 * h.w1, iw2 = I1 * h.w2;
     double ct0 = -cross_c(h.w1, iw2, h.w2, iw1), ct1 = -cross_c(h.w2, iw0, h.w0, iw2),
@@ -300,6 +308,13 @@ SD void step_b(HotB& h, const Params& P, const PreB& g) {
     const double nal2 = qdiv(sm_mad(-ir2, h.w2, (h.jt2 + dt2) + ct2) + amt2, rI1);
     h.al0 = nal0; h.al1 = nal1; h.al2 = nal2;
     h.w0 = sm_mad(nal0, DT, h.w0); h.w1 = sm_mad(nal1, DT, h.w1); h.w2 = sm_mad(nal2, DT, h.w2);
+}
+/* The rest of wave B's tick: Euler-angle and angle integration, the clock and
+ * shape-side properties committed, roll / pitch sin/cos at the new angles (and
+ * the yaw's for wave A when YAW). */
+template <int MODE, bool YAW = true>
+SD void step_b2(HotB& h, const Params& P, const PreB& g) {
+    constexpr bool STEADY = MODE != PM_FULL;
     {
         const Rcp rc = rcp_of(h.cth);
         double tt = qdiv(h.st, rc);
@@ -318,11 +333,24 @@ SD void step_b(HotB& h, const Params& P, const PreB& g) {
         h.dimx = g.ng.dimx; h.dimy = g.ng.dimy;
     }
     sincos2_p(h.e0, h.e1, &h.sp, &h.cp, &h.st, &h.cth, P.sk);
-    sm_sincos_nb_p(h.e2, &h.ss, &h.cs, P.sk);   /* yaw: wave A's world-frame update */
+    if (YAW) sm_sincos_nb_p(h.e2, &h.ss, &h.cs, P.sk);   /* yaw: wave A's world-frame update */
+}
+template <int MODE>
+SD void step_b(HotB& h, const Params& P, const PreB& g) {
+    step_b1<MODE>(h, P);
+    step_b2<MODE>(h, P, g);
 }
 template <int MODE>
 SD void step_b(HotB& h, const Params& P, Cache32 c32) {
     step_b<MODE>(h, P, pre_b<MODE>(h, P, c32));
+}
+
+/* SALP_PAIR_SPLIT's world-frame update of the tick just done on wave A: the
+ * yaw's sin/cos from the new yaw wave B sent, R at the new angles, p += (R v) dt
+ * (tick()'s to_world_frame_jit block). */
+SD void a_world_yaw(HotA& h, const Params& P, double yaw) {
+    sm_sincos_nb_p(yaw, &h.ss, &h.cs, P.sk);
+    a_world(h, P);
 }
 
 /* ---------------------------------------- LDS slot <-> the two waves */
