@@ -834,7 +834,7 @@ struct PairShared {
     int64_t steps[kPairEnvs];
     int16_t slot[2][kPairEnvs];
     uint64_t mask[2][2], amask[2][2];
-    int cnt[2][3];                            // [group][A, B (SALP_PAIR_SPLIT: B's first), B's second]: packets published
+    int cnt[2][2];                            // [group][role]: packets published
     int mode[2][2];                           // [group][buffer]: the tick kind wave A sent
     uint8_t flags[kPairEnvs];
 };
@@ -856,6 +856,8 @@ struct PairJobs {
     int done[2];                   // [group]: boundaries whose jobs are all published (chunk index + 1)
 };
 
+// Polls with s_sleep 1 (64 cycles) between them: s_sleep 0, 2 or none measured
+// the same, 4 slower (profiles/r4_experiments.md r4t).
 __device__ __forceinline__ bool pair_wait(int* flag, int target) {
     for (int it = 0; it < kPairSpin; ++it) {
         if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
@@ -866,69 +868,6 @@ __device__ __forceinline__ bool pair_wait(int* flag, int target) {
 }
 __device__ __forceinline__ void pair_publish(int* flag, int value) {
     __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// SALP_PAIR_FASTSYNC=1: the packet protocol on LDS's in-order execution of a
-// wave's DS instructions instead of release / acquire: the writer stores the
-// data and then the counter as volatile LDS stores (program order, no wait
-// for the data stores to land), the reader loads the counter and the data in
-// one round (the counter load executes first) and keeps the data once the
-// counter shows the packet.  One LDS round trip per receive instead of two,
-// no store-completion wait per publish.
-#ifndef SALP_PAIR_FASTSYNC
-#define SALP_PAIR_FASTSYNC 0
-#endif
-// SALP_PAIR_PREFETCH=1: a full tick's clock / phase / geometry (salp_pair.h
-// pre_a, pre_b: no partner data) computed between publishing a packet and
-// waiting for the partner's, so that it fills the wait; wave B computes it
-// speculatively after a full tick (the next is full too until the chunk's full
-// ticks end).
-#ifndef SALP_PAIR_PREFETCH
-#define SALP_PAIR_PREFETCH 0
-#endif
-
-template <class F>
-__device__ __forceinline__ bool pair_wait_read(int* flag, int target, F read) {
-    for (int it = 0; it < kPairSpin; ++it) {
-        const int f = __builtin_amdgcn_readfirstlane(*(volatile int*)flag);
-        read();
-        if (f >= target) return true;
-    }
-    if ((threadIdx.x & 63) == 0) atomicAdd(&g_pair_timeouts, 1u);
-    return false;
-}
-
-// SALP_PAIR_SPLIT=1: wave B sends two packets per tick instead of one.  The
-// first (new angular velocity, angular accelerations y, z) right after Euler's
-// equations, which is all wave A's next Newton step needs; the second (roll /
-// pitch sin/cos at the new angles, the new yaw, the drag-force coefficients)
-// after the angle integration, sin/cos and geometry, which wave A needs only
-// for the world-frame update of the tick just done (now after its next packet
-// went out) and its next Newton step.  Wave A computes the yaw's sin/cos
-// itself (its share of the tick was the lighter one).  The two waves' critical
-// loop is then Newton <-> Euler; the rest of each half overlaps the partner.
-#ifndef SALP_PAIR_SPLIT
-#define SALP_PAIR_SPLIT 0
-#endif
-// A packet out / in, with either protocol (SALP_PAIR_FASTSYNC or
-// release / acquire).  write(o) / read(q) store / load the packet's doubles
-// through o / q (volatile pointers under FASTSYNC).
-template <class W>
-__device__ __forceinline__ void xch_put(double* o, int* cnt, int value, W write) {
-    if (SALP_PAIR_FASTSYNC) {
-        write((volatile double*)o);
-        *(volatile int*)cnt = value;
-    } else {
-        write(o);
-        pair_publish(cnt, value);
-    }
-}
-template <class R>
-__device__ __forceinline__ bool xch_get(const double* q, int* cnt, int target, R read) {
-    if (SALP_PAIR_FASTSYNC) return pair_wait_read(cnt, target, [&] { read((volatile const double*)q); });
-    const bool ok = pair_wait(cnt, target);
-    read(q);
-    return ok;
 }
 
 struct ValuesToPartner {
@@ -1067,7 +1006,7 @@ __device__ __forceinline__ void pair_wave_a(PairShared& sh, PairJobs* jobs, cons
             salp::fill_cache32(P, h.c, salp::Cache32{sh.cache32 + s, kPairEnvs});
         }
         salp::spill<false>(h, salp::SpillSlot{sh.big + s, kPairEnvs});
-        if (lane < 3) sh.cnt[grp][lane] = 0;
+        if (lane < 2) sh.cnt[grp][lane] = 0;
         if (POL && lane == 0) {
             jobs->cnt[grp] = 0;
             jobs->done[grp] = 0;
@@ -1168,96 +1107,26 @@ __device__ __forceinline__ void pair_wave_a(PairShared& sh, PairJobs* jobs, cons
             const auto publish = [&](int mode) {
                 double X[3], jt[2];
                 salp::a_prepare(h, PV, X, jt);
-                if (SALP_PAIR_FASTSYNC) {
-                    volatile double* const o = ab + (pub & 1) * kXchAB * 64;
-                    o[0 * 64] = X[0]; o[1 * 64] = X[1]; o[2 * 64] = X[2]; o[3 * 64] = jt[0]; o[4 * 64] = jt[1];
-                    ((volatile int*)sh.mode[grp])[pub & 1] = mode;
-                    *(volatile int*)&sh.cnt[grp][0] = ++pub;
-                } else {
-                    double* const o = ab + (pub & 1) * kXchAB * 64;
-                    o[0 * 64] = X[0]; o[1 * 64] = X[1]; o[2 * 64] = X[2]; o[3 * 64] = jt[0]; o[4 * 64] = jt[1];
-                    if (lane == 0) sh.mode[grp][pub & 1] = mode;
-                    pair_publish(&sh.cnt[grp][0], ++pub);
-                }
+                double* const o = ab + (pub & 1) * kXchAB * 64;
+                o[0 * 64] = X[0]; o[1 * 64] = X[1]; o[2 * 64] = X[2]; o[3 * 64] = jt[0]; o[4 * 64] = jt[1];
+                if (lane == 0) sh.mode[grp][pub & 1] = mode;
+                pair_publish(&sh.cnt[grp][0], ++pub);
             };
             bool ok = true;
             const auto recv = [&]() {
                 prof.lap(PP_PUBLISH);
-                if (SALP_PAIR_FASTSYNC) {
-                    volatile const double* const q = ba + (rcv & 1) * kXchBA * 64;
-                    ok = pair_wait_read(&sh.cnt[grp][1], rcv + 1, [&] {
-                        h.w0 = q[0 * 64]; h.w1 = q[1 * 64]; h.w2 = q[2 * 64]; h.al1 = q[3 * 64]; h.al2 = q[4 * 64];
-                        h.sp = q[5 * 64]; h.cp = q[6 * 64]; h.st = q[7 * 64]; h.cth = q[8 * 64]; h.ss = q[9 * 64];
-                        h.cs = q[10 * 64]; h.kc0 = q[11 * 64]; h.kc1 = q[12 * 64];
-                    }) && ok;
-                    prof.lap(PP_WAIT);
-                } else {
-                    ok = pair_wait(&sh.cnt[grp][1], rcv + 1) && ok;
-                    prof.lap(PP_WAIT);
-                    const double* const q = ba + (rcv & 1) * kXchBA * 64;
-                    h.w0 = q[0 * 64]; h.w1 = q[1 * 64]; h.w2 = q[2 * 64]; h.al1 = q[3 * 64]; h.al2 = q[4 * 64];
-                    h.sp = q[5 * 64]; h.cp = q[6 * 64]; h.st = q[7 * 64]; h.cth = q[8 * 64]; h.ss = q[9 * 64];
-                    h.cs = q[10 * 64]; h.kc0 = q[11 * 64]; h.kc1 = q[12 * 64];
-                }
+                ok = pair_wait(&sh.cnt[grp][1], rcv + 1) && ok;
+                prof.lap(PP_WAIT);
+                const double* const q = ba + (rcv & 1) * kXchBA * 64;
+                h.w0 = q[0 * 64]; h.w1 = q[1 * 64]; h.w2 = q[2 * 64]; h.al1 = q[3 * 64]; h.al2 = q[4 * 64];
+                h.sp = q[5 * 64]; h.cp = q[6 * 64]; h.st = q[7 * 64]; h.cth = q[8 * 64]; h.ss = q[9 * 64];
+                h.cs = q[10 * 64]; h.kc0 = q[11 * 64]; h.kc1 = q[12 * 64];
                 ++rcv;
                 prof.lap(PP_READ);
             };
             prof.lap(PP_BOUNDARY);
             int mode = decide();
-            if (SALP_PAIR_SPLIT) {
-                double* const b1p = ba;                 // wave B's first packets: 2 x 5 doubles
-                double* const b2p = ba + 2 * 5 * 64;    // its second packets: 2 x 7 doubles
-                const auto put = [&](int md) {
-                    double X[3], jt[2];
-                    salp::a_prepare(h, PV, X, jt);
-                    const int b = pub & 1;
-                    xch_put(ab + b * kXchAB * 64, &sh.cnt[grp][0], pub + 1, [&](auto o) {
-                        o[0 * 64] = X[0]; o[1 * 64] = X[1]; o[2 * 64] = X[2]; o[3 * 64] = jt[0]; o[4 * 64] = jt[1];
-                        if (lane == 0) ((volatile int*)sh.mode[grp])[b] = md;
-                    });
-                    ++pub;
-                };
-                put(mode);
-                int rcv2 = rcv;   // B's second packets so far: one per tick, like its first
-                while (mode != salp::PM_END && ok) {
-                    const bool ticks = h.ct < h.b2;
-                    if (mode == salp::PM_FULL) {
-                        if (ticks) salp::step_a_newton<salp::PM_FULL>(h, PV, salp::pre_a<salp::PM_FULL>(h, PV, c32));
-                    } else if (mode == salp::PM_STEADY) {
-                        bool settled = true;
-                        if (ticks)
-                            settled = salp::step_a_newton<salp::PM_STEADY>(h, PV,
-                                                                           salp::pre_a<salp::PM_STEADY>(h, PV, c32));
-                        if (__all(settled)) stage = 2;
-                    } else {
-                        if (ticks)
-                            salp::step_a_newton<salp::PM_SETTLED>(h, PV, salp::pre_a<salp::PM_SETTLED>(h, PV, c32));
-                    }
-                    mode = decide();
-                    prof.lap(PP_TICK);
-                    put(mode);
-                    prof.lap(PP_PUBLISH);
-                    double yaw = 0.0;
-                    ok = xch_get(b2p + (rcv2 & 1) * 7 * 64, &sh.cnt[grp][2], rcv2 + 1, [&](auto q) {
-                        h.sp = q[0 * 64]; h.cp = q[1 * 64]; h.st = q[2 * 64]; h.cth = q[3 * 64]; yaw = q[4 * 64];
-                        h.kc0 = q[5 * 64]; h.kc1 = q[6 * 64];
-                    }) && ok;
-                    ++rcv2;
-                    prof.lap(PP_WAIT);
-                    if (ticks) salp::a_world_yaw(h, PV, yaw);
-                    prof.lap(PP_WORLD);
-                    if (mode != salp::PM_END)
-                        ok = xch_get(b1p + (rcv & 1) * 5 * 64, &sh.cnt[grp][1], rcv + 1, [&](auto q) {
-                            h.w0 = q[0 * 64]; h.w1 = q[1 * 64]; h.w2 = q[2 * 64]; h.al1 = q[3 * 64]; h.al2 = q[4 * 64];
-                        }) && ok;
-                    ++rcv;   // counted at the end of the chunk too: wave B sent that packet
-                    prof.lap(PP_WAIT);
-                }
-                rcv = rcv2;
-            } else {
             publish(mode);
-            salp::PreA pre{};
-            if (SALP_PAIR_PREFETCH && mode == salp::PM_FULL) pre = salp::pre_a<salp::PM_FULL>(h, PV, c32);
             recv();
             // pend: the lane's last tick still owes its world-frame position
             // update (step_a does it at the start of the next tick, with the
@@ -1266,9 +1135,7 @@ __device__ __forceinline__ void pair_wave_a(PairShared& sh, PairJobs* jobs, cons
             while (mode != salp::PM_END && ok) {
                 const bool ticks = h.ct < h.b2;
                 if (mode == salp::PM_FULL) {
-                    if (ticks)
-                        salp::step_a<salp::PM_FULL>(h, PV, SALP_PAIR_PREFETCH ? pre : salp::pre_a<salp::PM_FULL>(h, PV, c32),
-                                                    pend);
+                    if (ticks) salp::step_a<salp::PM_FULL>(h, PV, c32, pend);
                 } else if (mode == salp::PM_STEADY) {
                     bool settled = true;
                     if (ticks) settled = salp::step_a<salp::PM_STEADY>(h, PV, c32, pend);
@@ -1280,12 +1147,10 @@ __device__ __forceinline__ void pair_wave_a(PairShared& sh, PairJobs* jobs, cons
                 mode = decide();
                 prof.lap(PP_TICK);
                 publish(mode);
-                if (SALP_PAIR_PREFETCH && mode == salp::PM_FULL) pre = salp::pre_a<salp::PM_FULL>(h, PV, c32);
                 recv();
             }
             if (pend) salp::a_world(h, PV);
             prof.lap(PP_WORLD);
-            }
         }
         prof.lap(PP_BOUNDARY);
         __syncthreads();   // #3: packets done
@@ -1344,104 +1209,34 @@ __device__ __forceinline__ void pair_wave_b(PairShared& sh, PairJobs* jobs, cons
             double* const ab = sh.big + grp * 2 * kXchAB * 64 + lane;
             double* const ba = sh.big + kXchBase + grp * 2 * kXchBA * 64 + lane;
             const auto publish = [&]() {
-                if (SALP_PAIR_FASTSYNC) {
-                    volatile double* const o = ba + (pub & 1) * kXchBA * 64;
-                    o[0 * 64] = h.w0; o[1 * 64] = h.w1; o[2 * 64] = h.w2; o[3 * 64] = h.al1; o[4 * 64] = h.al2;
-                    o[5 * 64] = h.sp; o[6 * 64] = h.cp; o[7 * 64] = h.st; o[8 * 64] = h.cth; o[9 * 64] = h.ss;
-                    o[10 * 64] = h.cs; o[11 * 64] = h.kc0; o[12 * 64] = h.kc1;
-                    *(volatile int*)&sh.cnt[grp][1] = ++pub;
-                } else {
-                    double* const o = ba + (pub & 1) * kXchBA * 64;
-                    o[0 * 64] = h.w0; o[1 * 64] = h.w1; o[2 * 64] = h.w2; o[3 * 64] = h.al1; o[4 * 64] = h.al2;
-                    o[5 * 64] = h.sp; o[6 * 64] = h.cp; o[7 * 64] = h.st; o[8 * 64] = h.cth; o[9 * 64] = h.ss;
-                    o[10 * 64] = h.cs; o[11 * 64] = h.kc0; o[12 * 64] = h.kc1;
-                    pair_publish(&sh.cnt[grp][1], ++pub);
-                }
+                double* const o = ba + (pub & 1) * kXchBA * 64;
+                o[0 * 64] = h.w0; o[1 * 64] = h.w1; o[2 * 64] = h.w2; o[3 * 64] = h.al1; o[4 * 64] = h.al2;
+                o[5 * 64] = h.sp; o[6 * 64] = h.cp; o[7 * 64] = h.st; o[8 * 64] = h.cth; o[9 * 64] = h.ss;
+                o[10 * 64] = h.cs; o[11 * 64] = h.kc0; o[12 * 64] = h.kc1;
+                pair_publish(&sh.cnt[grp][1], ++pub);
             };
             // a bound on the ticks of one chunk (A ends it earlier)
             const int64_t cap = 4 + (int64_t)A.chunk + (((int64_t)A.chunk * A.steady_q8) >> 8);
             prof.lap(PP_BOUNDARY);
-            if (SALP_PAIR_SPLIT) {
-                double* const b1p = ba;
-                double* const b2p = ba + 2 * 5 * 64;
-                for (int64_t it = 0; it < cap; ++it) {
-                    int mv = 0;
-                    const int b = rcv & 1;
-                    const bool ok = xch_get(ab + b * kXchAB * 64, &sh.cnt[grp][0], rcv + 1, [&](auto q) {
-                        h.X0 = q[0 * 64]; h.X1 = q[1 * 64]; h.X2 = q[2 * 64]; h.jt1 = q[3 * 64]; h.jt2 = q[4 * 64];
-                        mv = ((volatile const int*)sh.mode[grp])[b];
-                    });
-                    const int mode = __builtin_amdgcn_readfirstlane(mv);
-                    ++rcv;
-                    prof.lap(PP_WAIT);
-                    if (mode == salp::PM_END || !ok) break;
-                    const bool ticks = h.ct < h.b2;
-                    if (ticks) {
-                        if (mode == salp::PM_FULL) salp::step_b1<salp::PM_FULL>(h, PV);
-                        else if (mode == salp::PM_STEADY) salp::step_b1<salp::PM_STEADY>(h, PV);
-                        else salp::step_b1<salp::PM_SETTLED>(h, PV);
-                    }
-                    prof.lap(PP_TICK);
-                    xch_put(b1p + (pub & 1) * 5 * 64, &sh.cnt[grp][1], pub + 1, [&](auto o) {
-                        o[0 * 64] = h.w0; o[1 * 64] = h.w1; o[2 * 64] = h.w2; o[3 * 64] = h.al1; o[4 * 64] = h.al2;
-                    });
-                    prof.lap(PP_PUBLISH);
-                    if (ticks) {
-                        if (mode == salp::PM_FULL)
-                            salp::step_b2<salp::PM_FULL, false>(h, PV, salp::pre_b<salp::PM_FULL>(h, PV, c32));
-                        else if (mode == salp::PM_STEADY)
-                            salp::step_b2<salp::PM_STEADY, false>(h, PV, salp::pre_b<salp::PM_STEADY>(h, PV, c32));
-                        else
-                            salp::step_b2<salp::PM_SETTLED, false>(h, PV, salp::pre_b<salp::PM_SETTLED>(h, PV, c32));
-                    }
-                    prof.lap(PP_TICK);
-                    xch_put(b2p + (pub & 1) * 7 * 64, &sh.cnt[grp][2], pub + 1, [&](auto o) {
-                        o[0 * 64] = h.sp; o[1 * 64] = h.cp; o[2 * 64] = h.st; o[3 * 64] = h.cth; o[4 * 64] = h.e2;
-                        o[5 * 64] = h.kc0; o[6 * 64] = h.kc1;
-                    });
-                    ++pub;
-                    prof.lap(PP_PUBLISH);
-                }
-            } else {
             publish();
             prof.lap(PP_PUBLISH);
-            bool prefetched = false;
-            salp::PreB pre{};
             for (int64_t it = 0; it < cap; ++it) {
-                bool ok;
-                int mode;
-                if (SALP_PAIR_FASTSYNC) {
-                    volatile const double* const q = ab + (rcv & 1) * kXchAB * 64;
-                    volatile const int* const qm = &sh.mode[grp][rcv & 1];
-                    int mv = 0;
-                    ok = pair_wait_read(&sh.cnt[grp][0], rcv + 1, [&] {
-                        h.X0 = q[0 * 64]; h.X1 = q[1 * 64]; h.X2 = q[2 * 64]; h.jt1 = q[3 * 64]; h.jt2 = q[4 * 64];
-                        mv = *qm;
-                    });
-                    mode = __builtin_amdgcn_readfirstlane(mv);
-                    prof.lap(PP_WAIT);
-                } else {
-                    ok = pair_wait(&sh.cnt[grp][0], rcv + 1);
-                    prof.lap(PP_WAIT);
-                    const double* const q = ab + (rcv & 1) * kXchAB * 64;
-                    h.X0 = q[0 * 64]; h.X1 = q[1 * 64]; h.X2 = q[2 * 64]; h.jt1 = q[3 * 64]; h.jt2 = q[4 * 64];
-                    mode = __builtin_amdgcn_readfirstlane(sh.mode[grp][rcv & 1]);
-                }
+                const bool ok = pair_wait(&sh.cnt[grp][0], rcv + 1);
+                prof.lap(PP_WAIT);
+                const double* const q = ab + (rcv & 1) * kXchAB * 64;
+                h.X0 = q[0 * 64]; h.X1 = q[1 * 64]; h.X2 = q[2 * 64]; h.jt1 = q[3 * 64]; h.jt2 = q[4 * 64];
+                const int mode = __builtin_amdgcn_readfirstlane(sh.mode[grp][rcv & 1]);
                 ++rcv;
                 prof.lap(PP_READ);
                 if (mode == salp::PM_END || !ok) break;
                 if (h.ct < h.b2) {
-                    if (mode == salp::PM_FULL)
-                        salp::step_b<salp::PM_FULL>(h, PV, prefetched ? pre : salp::pre_b<salp::PM_FULL>(h, PV, c32));
+                    if (mode == salp::PM_FULL) salp::step_b<salp::PM_FULL>(h, PV, c32);
                     else if (mode == salp::PM_STEADY) salp::step_b<salp::PM_STEADY>(h, PV, c32);
                     else salp::step_b<salp::PM_SETTLED>(h, PV, c32);
                 }
                 prof.lap(PP_TICK);
                 publish();
                 prof.lap(PP_PUBLISH);
-                prefetched = SALP_PAIR_PREFETCH && mode == salp::PM_FULL;
-                if (prefetched) pre = salp::pre_b<salp::PM_FULL>(h, PV, c32);   // the next tick, if full
-            }
             }
         }
         prof.lap(PP_BOUNDARY);

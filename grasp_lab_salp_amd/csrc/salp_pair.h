@@ -126,8 +126,8 @@ SD void a_world(HotA& h, const Params&) {
  * for wave A.  Every value is the expression tick() computes. */
 
 /* A tick's clock, phase and (full ticks) mass-side geometry: a function of
- * wave A's own state alone, so it can be computed before the partner's
- * packet arrives (SALP_PAIR_PREFETCH). */
+ * wave A's own state alone.  (Computing it between publishing and waiting,
+ * to fill the wait, measured slower: profiles/r4_experiments.md r4s.) */
 struct PreA {
     double ct, L, W, V, com, comr, coma, m, mr, speed, rm;
     int phase;
@@ -310,9 +310,9 @@ SD void step_b1(HotB& h, const Params& P) {
     h.w0 = sm_mad(nal0, DT, h.w0); h.w1 = sm_mad(nal1, DT, h.w1); h.w2 = sm_mad(nal2, DT, h.w2);
 }
 /* The rest of wave B's tick: Euler-angle and angle integration, the clock and
- * shape-side properties committed, roll / pitch sin/cos at the new angles (and
- * the yaw's for wave A when YAW). */
-template <int MODE, bool YAW = true>
+ * shape-side properties committed, roll / pitch / yaw sin/cos at the new
+ * angles (the yaw's for wave A). */
+template <int MODE>
 SD void step_b2(HotB& h, const Params& P, const PreB& g) {
     constexpr bool STEADY = MODE != PM_FULL;
     {
@@ -333,7 +333,7 @@ SD void step_b2(HotB& h, const Params& P, const PreB& g) {
         h.dimx = g.ng.dimx; h.dimy = g.ng.dimy;
     }
     sincos2_p(h.e0, h.e1, &h.sp, &h.cp, &h.st, &h.cth, P.sk);
-    if (YAW) sm_sincos_nb_p(h.e2, &h.ss, &h.cs, P.sk);   /* yaw: wave A's world-frame update */
+    sm_sincos_nb_p(h.e2, &h.ss, &h.cs, P.sk);   /* yaw: wave A's world-frame update */
 }
 template <int MODE>
 SD void step_b(HotB& h, const Params& P, const PreB& g) {
@@ -345,13 +345,6 @@ SD void step_b(HotB& h, const Params& P, Cache32 c32) {
     step_b<MODE>(h, P, pre_b<MODE>(h, P, c32));
 }
 
-/* SALP_PAIR_SPLIT's world-frame update of the tick just done on wave A: the
- * yaw's sin/cos from the new yaw wave B sent, R at the new angles, p += (R v) dt
- * (tick()'s to_world_frame_jit block). */
-SD void a_world_yaw(HotA& h, const Params& P, double yaw) {
-    sm_sincos_nb_p(yaw, &h.ss, &h.cs, P.sk);
-    a_world(h, P);
-}
 
 /* ---------------------------------------- LDS slot <-> the two waves */
 /* The spill slot (salp_device.h spill / unspill, non-RAND layout) is the
