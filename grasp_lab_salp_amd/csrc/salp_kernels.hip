@@ -275,27 +275,44 @@ constexpr int kPH = SALP_POLICY_HIDDEN, kPIN = SALP_OBS_DIM_MAX;
 // 26.7 M env-steps/s at 65 536 envs, profiles/r2_experiments.md r2u).
 typedef const __attribute__((address_space(4))) float* PolicyW;
 
+// Two hidden units per instruction: v_pk_fma_f32 (packed fp32, two IEEE fmas,
+// each unit's sum in the same order as one fmaf chain, so the same bits) with
+// the pair of weights as an SGPR pair and the input broadcast by op_sel.
+typedef float PolicyF2 __attribute__((ext_vector_type(2)));
+static_assert(kPH % 2 == 0, "hidden units go in pairs");
+
 template <int NOUT>
 __device__ __forceinline__ void policy_mlp(PolicyW w, int w1, int b1, int w2, int b2, int hw,
                                            int hb, const float* x, float* out) {
     float h1[kPH];
 #pragma unroll
-    for (int j = 0; j < kPH; ++j) {
-        float acc = w[b1 + j];
+    for (int j = 0; j < kPH; j += 2) {
+        PolicyF2 acc = {w[b1 + j], w[b1 + j + 1]};
 #pragma unroll
-        for (int k = 0; k < kPIN; ++k) acc = fmaf(w[w1 + j * kPIN + k], x[k], acc);
-        h1[j] = tanhf(acc);
+        for (int k = 0; k < kPIN; ++k) {
+            const PolicyF2 wk = {w[w1 + j * kPIN + k], w[w1 + (j + 1) * kPIN + k]};
+            const PolicyF2 xk = {x[k], x[k]};
+            acc = __builtin_elementwise_fma(wk, xk, acc);
+        }
+        h1[j] = tanhf(acc.x);
+        h1[j + 1] = tanhf(acc.y);
     }
 #pragma unroll
     for (int c = 0; c < NOUT; ++c) out[c] = 0.0f;
 #pragma unroll 1
-    for (int j = 0; j < kPH; ++j) {
-        float acc = w[b2 + j];
+    for (int j = 0; j < kPH; j += 2) {
+        PolicyF2 acc = {w[b2 + j], w[b2 + j + 1]};
 #pragma unroll
-        for (int k = 0; k < kPH; ++k) acc = fmaf(w[w2 + j * kPH + k], h1[k], acc);
-        const float t = tanhf(acc);
+        for (int k = 0; k < kPH; ++k) {
+            const PolicyF2 wk = {w[w2 + j * kPH + k], w[w2 + (j + 1) * kPH + k]};
+            const PolicyF2 hk = {h1[k], h1[k]};
+            acc = __builtin_elementwise_fma(wk, hk, acc);
+        }
+        const float t0 = tanhf(acc.x), t1 = tanhf(acc.y);
 #pragma unroll
-        for (int c = 0; c < NOUT; ++c) out[c] = fmaf(w[hw + c * kPH + j], t, out[c]);
+        for (int c = 0; c < NOUT; ++c) out[c] = fmaf(w[hw + c * kPH + j], t0, out[c]);
+#pragma unroll
+        for (int c = 0; c < NOUT; ++c) out[c] = fmaf(w[hw + c * kPH + j + 1], t1, out[c]);
     }
 #pragma unroll
     for (int c = 0; c < NOUT; ++c) out[c] += w[hb + c];
