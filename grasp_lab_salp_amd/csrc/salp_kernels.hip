@@ -1801,14 +1801,18 @@ int salp_collect(SalpEnv* h, const SalpPolicyRollout* r, void* stream) {
     b.max_steps = r->n_steps;
     // Longer chunks than the rollout's 128: every wave evaluates the policy at
     // most once per chunk, and that evaluation is on its critical path
-    // (65 536 envs, M env-steps/s by chunk 128 / 192 / 256 / 384 / 512 / 768:
-    // 26.3 / 28.3 / 28.3 / 29.2 / 28.6 / 24.6; profiles/r2_experiments.md r2x).
-    // SALP_COLLECT_CHUNK overrides it for tuning runs.
-    static const int32_t chunk = [] {
+    // (k_rollout, 65 536 envs, M env-steps/s by chunk 128 / 192 / 256 / 384 /
+    // 512 / 768: 26.3 / 28.3 / 28.3 / 29.2 / 28.6 / 24.6; profiles/
+    // r2_experiments.md r2x).  k_rollout_pair, whose B wave takes the value
+    // network off the A wave's boundary: 192 (32 768 envs, chunk 96 / 128 / 160
+    // / 192 / 224 / 256 / 384: 20.2 / 21.3 / 21.5 / 21.9 / 21.6 / 21.2 / 20.9;
+    // profiles/r4_experiments.md r4x).  SALP_COLLECT_CHUNK overrides both.
+    static const int32_t forced_chunk = [] {
         const char* e = std::getenv("SALP_COLLECT_CHUNK");
         const long v = e ? std::strtol(e, nullptr, 10) : 0;
-        return (int32_t)(v > 0 && v < 4096 ? v : 384);
+        return (int32_t)(v > 0 && v < 4096 ? v : 0);
     }();
+    const int32_t chunk = forced_chunk ? forced_chunk : use_pair(h) ? 192 : 384;
     const int64_t n_chunks = (r->n_steps * kMaxTicksPerCycle + chunk - 1) / chunk;
     RolloutArgs args{h->state, h->dp, n_chunks, chunk, rollout_steady_q8(), r->n_steps, b, nullptr, 1, 0, *r};
     return launch_chained(h, args, true, st, "k_rollout(collect)");
