@@ -74,9 +74,37 @@ def kernel_symbols(lib_path, contains):
     return sorted(names)
 
 
+def _mask_layout(code):
+    """The kernel's machine code with the bytes that only say where things lie
+    in the code object zeroed: the 32-bit literal of each `s_add_u32` /
+    `s_addc_u32` that follows an `s_getpc_b64` (a PC-relative address of a
+    global or a callee, which moves when anything else in the library grows or
+    shrinks).  Everything else, branch offsets inside the kernel included, is
+    kept."""
+    n = len(code) // 4
+    w = list(struct.unpack("<%dI" % n, code[:4 * n]))
+    for i in range(n):
+        if (w[i] & 0xFF80FFFF) != 0xBE801C00:       # s_getpc_b64 s[k:k+1]
+            continue
+        j = i + 1
+        while j + 1 < n and j <= i + 4:
+            op = w[j] & 0xFF800000
+            lit = (w[j] & 0xFF) == 0xFF or (w[j] >> 8 & 0xFF) == 0xFF
+            if op in (0x80000000, 0x82000000) and lit:   # s_add_u32 / s_addc_u32 with a literal
+                w[j + 1] = 0
+                j += 2
+            else:
+                j += 1
+    return struct.pack("<%dI" % n, *w) + code[4 * n:]
+
+
 def kernel_sha(lib_path, contains):
     """sha256 (hex, 16 chars) of the code + descriptor of the one kernel whose
-    mangled name contains `contains`, or None (absent or ambiguous)."""
+    mangled name contains `contains`, or None (absent or ambiguous).  Layout
+    bytes are masked (`_mask_layout`; the descriptor's
+    kernel_code_entry_byte_offset, bytes 16-23), so the fingerprint changes
+    with the kernel's own instructions, not with edits elsewhere in the
+    library."""
     blob = open(lib_path, "rb").read()
     for _ident, co in _code_objects(blob):
         syms = _symbols(co)
@@ -84,10 +112,12 @@ def kernel_sha(lib_path, contains):
         if len(hits) == 1:
             symbol = hits[0]
             h = hashlib.sha256()
-            for name in (symbol, symbol + ".kd"):
-                if name in syms:
-                    off, size = syms[name]
-                    h.update(co[off:off + size])
+            off, size = syms[symbol]
+            h.update(_mask_layout(co[off:off + size]))
+            off, size = syms[symbol + ".kd"]
+            kd = bytearray(co[off:off + size])
+            kd[16:24] = bytes(8)
+            h.update(bytes(kd))
             return h.hexdigest()[:16]
     return None
 

@@ -45,3 +45,24 @@ def test_bench_reports_pmc_only_for_the_measured_build(lib, tmp_path, monkeypatc
     json.dump({**base, "kernel_sha16": sha}, open(prof / "r9b_pmc_summary.json", "w"))
     name, summ, why = bench.pmc_profile(64, 32, 16)
     assert name == "r9b_pmc_summary.json" and why is None and summ["derived"]["hbm_bytes"] == 1.0
+
+
+def test_layout_mask_zeroes_only_pc_relative_literals():
+    """_mask_layout zeroes the literals of the s_add_u32 / s_addc_u32 pair after
+    an s_getpc_b64 (addresses that move with the rest of the library) and
+    nothing else, so an instruction change still changes the fingerprint."""
+    import struct
+    getpc = 0xBE821C00                     # s_getpc_b64 s[2:3]
+    add, addc = 0x8002FF02, 0x8203FF03     # s_add_u32 s2, s2, lit ; s_addc_u32 s3, s3, lit
+    other = 0xD2800000                     # some VOP3 word
+    words = [other, getpc, add, 0x1234, addc, 0x5, other, add, 0x777]
+    code = struct.pack("<%dI" % len(words), *words)
+    masked = struct.unpack("<%dI" % len(words), _codeobj._mask_layout(code))
+    # the pair after getpc is masked; an s_add_u32 literal elsewhere is not
+    assert masked == (other, getpc, add, 0, addc, 0, other, add, 0x777)
+    moved = list(words)
+    moved[3], moved[5] = 0x9999, 0x6
+    assert _codeobj._mask_layout(struct.pack("<9I", *moved)) == _codeobj._mask_layout(code)
+    changed = list(words)
+    changed[6] = other + 1
+    assert _codeobj._mask_layout(struct.pack("<9I", *changed)) != _codeobj._mask_layout(code)
