@@ -401,6 +401,19 @@ struct ValuesInPlace {
     __device__ __forceinline__ void publish() {}
 };
 
+// salp_collect: a further round of env-step boundaries within one chunk
+// boundary runs only when at least this many lanes of the wave need it.  A
+// clipped action of 0 for the contraction and the coast time gives a cycle of
+// zero ticks, so under a fresh policy (mean ~0, std 1: half of each action
+// component clipped) many boundaries would otherwise run the whole wave's
+// policy evaluation again and again for a few lanes; those lanes now wait for
+// the next chunk boundary (per-env results unchanged).  PPO leg 15.6 -> 16.1 M
+// env-steps/s with 4 (1 / 4 / 8 / 16 / 64 measured; profiles/r4_experiments.md
+// r4rep).
+#ifndef SALP_COLLECT_REP_MIN
+#define SALP_COLLECT_REP_MIN 4
+#endif
+
 // torch.clamp(a, low, high): NaN stays NaN
 __device__ __forceinline__ float clamp_box(float a, float lo, float hi) { return a < lo ? lo : (a > hi ? hi : a); }
 
@@ -535,6 +548,13 @@ __device__ __forceinline__ void rollout_boundary(Hot& h, ST S, const Params& P, 
             }
             salp::begin_step<RAND>(h, S, P, i, a[0], a[1], a[2], c32);
             pending = true;
+        }
+        if (POL && SALP_COLLECT_REP_MIN > 1) {
+            // another round evaluates the policy for the whole wave again: run it
+            // only for enough lanes whose new cycle already ended (zero-tick
+            // cycles); the others finish that step at the next chunk boundary
+            const bool again = active && pending && !(h.ct < h.b2);
+            if (__popcll(__ballot(again)) < SALP_COLLECT_REP_MIN) break;
         }
         if (VS::kDefer) {   // the partner follows rep by rep: the wave leaves together
             if (!__any(fin || beg)) break;
