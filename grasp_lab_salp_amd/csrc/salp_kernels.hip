@@ -275,9 +275,13 @@ constexpr int kPH = SALP_POLICY_HIDDEN, kPIN = SALP_OBS_DIM_MAX;
 // 26.7 M env-steps/s at 65 536 envs, profiles/r2_experiments.md r2u).
 typedef const __attribute__((address_space(4))) float* PolicyW;
 
-// Two hidden units per instruction: v_pk_fma_f32 (packed fp32, two IEEE fmas,
-// each unit's sum in the same order as one fmaf chain, so the same bits) with
-// the pair of weights as an SGPR pair and the input broadcast by op_sel.
+// Packed fp32 (v_pk_fma_f32: two IEEE fmas per instruction, the weight pair
+// an SGPR pair).  First layer: two hidden units per instruction, the input
+// broadcast by op_sel.  Second layer: one row at a time, its even and odd
+// inputs summed in the two halves, so that the row's 64 weights arrive as 32
+// aligned SGPR pairs of one scalar-load burst (profiles/r4_experiments.md r4kp;
+// float32 sums in another order than torch's, held to the torch policy by the
+// collection tests).
 typedef float PolicyF2 __attribute__((ext_vector_type(2)));
 static_assert(kPH % 2 == 0, "hidden units go in pairs");
 
@@ -318,19 +322,18 @@ __device__ __forceinline__ void policy_mlp(PolicyW w, int w1, int b1, int w2, in
 #pragma unroll
     for (int c = 0; c < NOUT; ++c) out[c] = 0.0f;
 #pragma unroll 1
-    for (int j = 0; j < kPH; j += 2) {
-        PolicyF2 acc = {w[b2 + j], w[b2 + j + 1]};
+    for (int j = 0; j < kPH; ++j) {
+        // one row: even and odd inputs in the two halves of a packed sum
+        PolicyF2 acc = {w[b2 + j], 0.0f};
 #pragma unroll
-        for (int k = 0; k < kPH; ++k) {
-            const PolicyF2 wk = {w[w2 + j * kPH + k], w[w2 + (j + 1) * kPH + k]};
-            const PolicyF2 hk = {h1[k], h1[k]};
+        for (int k = 0; k < kPH; k += 2) {
+            const PolicyF2 wk = {w[w2 + j * kPH + k], w[w2 + j * kPH + k + 1]};
+            const PolicyF2 hk = {h1[k], h1[k + 1]};
             acc = __builtin_elementwise_fma(wk, hk, acc);
         }
-        const float t0 = policy_tanh(acc.x), t1 = policy_tanh(acc.y);
+        const float t = policy_tanh(acc.x + acc.y);
 #pragma unroll
-        for (int c = 0; c < NOUT; ++c) out[c] = fmaf(w[hw + c * kPH + j], t0, out[c]);
-#pragma unroll
-        for (int c = 0; c < NOUT; ++c) out[c] = fmaf(w[hw + c * kPH + j + 1], t1, out[c]);
+        for (int c = 0; c < NOUT; ++c) out[c] = fmaf(w[hw + c * kPH + j], t, out[c]);
     }
 #pragma unroll
     for (int c = 0; c < NOUT; ++c) out[c] += w[hb + c];
