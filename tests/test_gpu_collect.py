@@ -10,7 +10,9 @@ The kernel's buffers are checked against an independent replay:
   observation, reward, episode start, guard reset, the final observations and
   the whole state bit for bit (up to NaN payloads);
 * rewards: SB3's timeout bootstrap gamma * V(terminal obs) where an episode
-  was truncated and not terminated, 0 where the divergence guard fired.
+  was truncated and not terminated, 0 where the divergence guard fired;
+* a policy that makes many zero-tick cycles (a boundary then leaves lanes to
+  the next chunk, SALP_COLLECT_REP_MIN) on both rollout kernels.
 """
 import numpy as np
 import pytest
@@ -54,8 +56,10 @@ def _equal_up_to_nan_payload(a, b):
 ALL_RAND = dict(dynamics=True, disturbances=True, actions=True, observations=True, latency=True)
 
 
-@pytest.mark.parametrize("n,n_steps,gamma,rand", [(300, 7, 0.99, False), (1024, 5, 0.9, False), (500, 6, 0.99, True)])
-def test_collect_replays_on_the_lockstep_path(n, n_steps, gamma, rand):
+@pytest.mark.parametrize("n,n_steps,gamma,rand,zero_tick,kernel", [
+    (300, 7, 0.99, False, False, -1), (1024, 5, 0.9, False, False, -1), (500, 6, 0.99, True, False, -1),
+    (700, 12, 0.99, False, True, 1), (700, 12, 0.99, False, True, 0)])
+def test_collect_replays_on_the_lockstep_path(n, n_steps, gamma, rand, zero_tick, kernel):
     """rand: every randomisation switch on (k_rollout<RAND, POL>; the twin's
     salp_step draws from the same Philox streams)."""
     p = default_params()
@@ -67,7 +71,16 @@ def test_collect_replays_on_the_lockstep_path(n, n_steps, gamma, rand):
         twin.set_randomization(**ALL_RAND)
     obs0 = env.reset()
     twin.set_state(env.get_state())
+    env.set_rollout_kernel(kernel)
     pol = _policy(1)
+    if zero_tick:
+        # contraction and coast clipped to 0 for about half the draws, the yaw
+        # near 0: many cycles of zero ticks, a few lanes at a time, so the
+        # boundary leaves most of them to the next chunk (SALP_COLLECT_REP_MIN)
+        with torch.no_grad():
+            pol.action_net.weight.mul_(0.01)
+            pol.action_net.bias.copy_(torch.tensor([0.0, 0.0, 0.0]))
+            pol.log_std.copy_(torch.tensor([-1.0, -1.0, -3.0]))
     w = pack_policy(pol)
     bufs = _buffers(n_steps, n, env.obs_dim)
     ep_start = torch.ones(n, dtype=torch.float32, device="cuda")
