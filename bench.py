@@ -59,6 +59,8 @@ BYTES_PER_ENV_STEP = 2 * STATE_BYTES + STEP_OUT_BYTES
 F_TICK_ALGO = 387
 # Mean ticks per env-step under the synthetic action distribution: the oracle
 # over 3 seeds x 4096 envs x 20 env-steps (245 760 env-steps) gives 710.4.
+# Only the fallback: a run with its parity check measures the mean of its own
+# replayed env-steps (parity_sampled.ticks_per_env_step) and uses that.
 MEAN_TICKS_PER_ENV_STEP = 710.4
 HOT_FIELDS = slice(FIELD["v0"], FIELD["ang2"] + 1)   # kinematic state: NaN once an env diverged
 
@@ -436,7 +438,15 @@ def main(argv=None):
     steps_per_launch = steps_local / a.steps
     bytes_launch = steps_per_launch * BYTES_PER_ENV_STEP
     achieved = bytes_launch / (kern_ms / 1e3) / 1e9
-    env_ticks_per_launch = steps_per_launch * MEAN_TICKS_PER_ENV_STEP
+    # ticks per env-step: measured on this run's own replayed env-steps when the
+    # parity check ran (rank 0's sample), else the oracle's 710.4
+    if parity is not None and parity.get("env_steps_replayed"):
+        tps, tps_src = parity["ticks_per_env_step"], (
+            f"measured: parity_sampled replayed {parity['env_steps_replayed']} completed env-steps of this run "
+            f"({parity['ticks_replayed']} ticks) on the oracle")
+    else:
+        tps, tps_src = MEAN_TICKS_PER_ENV_STEP, "constant: the oracle's mean over 245 760 random-action env-steps"
+    env_ticks_per_launch = steps_per_launch * tps
     res = {
         "metric": METRIC,
         "value": steps_total / elapsed,
@@ -458,10 +468,16 @@ def main(argv=None):
         "finite_env_steps_per_sec": finite_total / elapsed,
         "finite_note": "env-steps of envs whose kinematic state was finite at the start and at the end of the timed "
                        "region (diverged envs carry NaN, as the reference's integrator does, and count in value)",
-        "estimated_ticks_per_sec": steps_total * MEAN_TICKS_PER_ENV_STEP / elapsed,
-        "estimated_ticks_note": "env-steps/s x 710.4, the oracle's mean ticks per env-step under random actions "
-                                "(not a measured tick count)",
-        "budget_ticks_per_sec": budget_ticks / elapsed,
+        "ticks_per_env_step": tps,
+        "ticks_per_env_step_source": tps_src,
+        "ticks_per_sec": steps_total * tps / elapsed,
+        "ticks_note": "ticks_per_sec = value x ticks_per_env_step: physics ticks (dt 0.01 s) of the completed "
+                      "env-steps per second",
+        "budget_full_tick_equivalents_per_sec": budget_ticks / elapsed,
+        "budget_note": "tick_budget counts full-tick equivalents: per chunk a wave runs k full ticks, then "
+                       "(chunk - k) x q / 256 steady ticks (q = 480, a steady tick costs ~0.55 of a full one), so "
+                       "a lane's executed ticks per launch exceed tick_budget by up to q / 256 = 1.875x; "
+                       "ticks_per_sec above this rate is expected, not a contradiction",
         "kernel_ms_per_launch": kern_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
@@ -488,7 +504,10 @@ def main(argv=None):
     fl_algo = F_TICK_ALGO * env_ticks_per_launch / (kern_ms / 1e3) / 1e12
     res["roofline_valu"] = {"bound": "fp64-valu", "achieved": fl_algo, "peak": FP64_VALU_PEAK_TFLOPS,
                             "unit": "TFLOP/s", "frac": fl_algo / FP64_VALU_PEAK_TFLOPS,
-                            "flops_per_env_tick": F_TICK_ALGO, "count": "algorithmic (DESIGN.md §5)"}
+                            "flops_per_env_tick": F_TICK_ALGO, "ticks_per_env_step": tps,
+                            "env_ticks_per_launch": env_ticks_per_launch,
+                            "count": "algorithmic (DESIGN.md §5) x env-ticks per launch (env-steps per launch x "
+                                     "ticks_per_env_step)"}
     if prof[1]:
         d = prof[1]["derived"]
         per = prof[1]["per_dispatch"]
@@ -499,7 +518,8 @@ def main(argv=None):
                              "SQ_INSTS_VALU_TRANS_F64") if k in per}
             res["roofline_valu"]["executed"] = {
                 "achieved": fl, "frac": fl / FP64_VALU_PEAK_TFLOPS,
-                "flops_per_env_tick": d.get("fp64_flops_per_env_tick"), "instruction_mix": mix,
+                "flops_per_budget_tick": d.get("fp64_flops_per_env_tick"),
+                "flops_per_env_tick": d["fp64_flops"] / env_ticks_per_launch, "instruction_mix": mix,
                 "active_valu_frac": d.get("active_valu_frac"), "waves": per.get("SQ_WAVES", {}).get("mean"),
                 "source": prof[0],
                 "note": "PMC fp64 VALU instructions x 64 lanes (FMA = 2): both arms of branch-free selects, "

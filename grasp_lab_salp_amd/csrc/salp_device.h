@@ -35,6 +35,12 @@
 
 #pragma clang fp contract(off)
 
+/* The device implements the product arithmetic mode only (salp_math.h
+ * SALP_FMA = 1: fused product-sums, the tick's sin / cos, world-frame
+ * rotation, Euler-rate map and reciprocal quotients); the oracle implements
+ * both, SALP_FMA = 0 being NumPy's own evaluation order. */
+static_assert(SALP_FMA, "libsalp.so is built in the product arithmetic mode (salp_math.h)");
+
 #define SD static __device__ __forceinline__
 #define SD_MEMBER __device__ __forceinline__
 #define SD_HOST_DEV static __host__ __device__ __forceinline__
@@ -148,24 +154,6 @@ SD float cubef(float x) {
     return r;
 }
 
-/* sm_sincos_p of two angles (a tick's roll and pitch): one wave-uniform test
- * and one straight-line path when every active lane takes the |x| <= pi/4 (or
- * NaN) arm of both, instead of two divergent if/else regions with a reduction
- * path each.  Bit-identical to two sm_sincos_p calls. */
-SD void sincos2_p(double x0, double x1, double* s0, double* c0, double* s1, double* c1, SmPoly K) {
-    const bool small0 = (sm_hi(x0) & 0x7fffffff) <= 0x3fe921fb || x0 != x0;
-    const bool small1 = (sm_hi(x1) & 0x7fffffff) <= 0x3fe921fb || x1 != x1;
-    if (__all(small0 && small1)) {
-        *s0 = sm_ksin_p(x0, 0.0, 0, K);
-        *c0 = sm_kcos_p(x0, 0.0, K);
-        *s1 = sm_ksin_p(x1, 0.0, 0, K);
-        *c1 = sm_kcos_p(x1, 0.0, K);
-    } else {
-        sm_sincos_p(x0, s0, c0, K);
-        sm_sincos_p(x1, s1, c1, K);
-    }
-}
-
 /* Rotation R = Rz(psi) Ry(theta) Rx(phi) (src/dynamics.py:34-58) from the
  * dgemm-order product with its zeros removed. */
 struct Rot { double r[3][3]; };
@@ -187,9 +175,15 @@ SD Rot rot_zyx(double phi, double theta, double psi) {
     sm_sincos(psi, &ss, &cs);
     return rot_sc(sp, cp, st, ct, ss, cs);
 }
-/* R @ v (dgemv order) */
-SD void rot_apply(const Rot& R, double v0, double v1, double v2, double* o) {
-    for (int i = 0; i < 3; ++i) o[i] = sm_fma(R.r[i][2], v2, sm_fma(R.r[i][0], v0, R.r[i][1] * v1));
+/* to_world_frame_jit (src/dynamics.py:34-58) of v at the angles (e0, e1, e2)
+ * as the tick computes it (salp_math.h: the roll / pitch pair and yaw sin /
+ * cos, three plane rotations); finish_step and the trace use it too, so that
+ * every world-frame vector equals the oracle's to_world_frame. */
+SD void world_frame(double e0, double e1, double e2, double v0, double v1, double v2, double* o, SmPoly K) {
+    double sp, cp, st, ct, ss, cs;
+    sm_sincos_rp2(e0, e1, &sp, &cp, &st, &ct, K);
+    sm_sincos_yaw_p(e2, &ss, &cs, K);
+    sm_world_frame(sp, cp, st, ct, ss, cs, v0, v1, v2, o);
 }
 /* R.T @ (d0, d1, 0) (transposed view order), components 0 and 1 */
 SD void rot_body_xy(const Rot& R, double d0, double d1, double* b0, double* b1) {
@@ -271,7 +265,7 @@ struct Geo {
     double dimx, dimy;            /* width**3, length**3 */
     double speed;                 /* jet speed (V - V_prev) / dt / A_nozzle */
     double rx;                    /* jet moment arm x */
-    double rm, rI0, rI1;          /* refined reciprocals of m, I0, I1 (geo_recips) */
+    double rm, rI0, rI1;          /* correctly rounded 1/m, 1/I0, 1/I1 (geo_recips) */
 };
 /* compute_cross_sectional_area_jit (src/geometry.py:67-75): A0 = area[0],
  * A1 = area[1] = area[2]; compute_drag_coefficient_jit (src/geometry.py:
@@ -351,13 +345,15 @@ SD void jet_rates(const Params& P, double V, double pV, double wm, bool g32, boo
     g.mr = b32 ? mr32 : mr64;
     g.speed = b32 ? sp32 : sp64;
 }
-/* The divisors of the dynamics' two divisions (F/m, tau/I): computed with the
- * geometry, so that a tick whose geometry is kept (steady body) keeps them too
- * instead of re-running three reciprocal chains. */
+/* The correctly rounded reciprocals 1/m, 1/I0, 1/I1 of the dynamics' two
+ * solves (F/m, tau/I; product mode: F * (1/m), the oracle's robot_newton /
+ * robot_euler): computed with the geometry, so that a tick whose geometry is
+ * kept (steady body) keeps them too. */
+SD double rcr(double d) { return qdiv(1.0, rcp_of(d)); }
 SD void geo_recips(Geo& g) {
-    g.rm = rcp_of(g.m).r;
-    g.rI0 = rcp_of(g.I0).r;
-    g.rI1 = rcp_of(g.I1).r;
+    g.rm = rcr(g.m);
+    g.rI0 = rcr(g.I0);
+    g.rI1 = rcr(g.I1);
 }
 SD Geo make_geo(const Params& P, const Core& c, double L, double W, double V, double pV, bool g32,
                 bool pv32, double wm) {
@@ -535,8 +531,7 @@ SD double& sref(ColdRegs<RAND>* C, const Params&, int64_t, int f) {
 SD void refresh_derived(Hot& h, const Params& P) {
     const Core c = core(h.L, h.W, h.g32);
     h.geo = make_geo(P, c, h.L, h.W, h.V, h.pV, h.g32, h.pv32, water_mass(P, h.V, h.g32));
-    sm_sincos(h.e0, &h.sp, &h.cp);
-    sm_sincos(h.e1, &h.st, &h.cth);
+    sm_sincos_rp2(h.e0, h.e1, &h.sp, &h.cp, &h.st, &h.cth, sm_poly());
 }
 
 /* the RAND-only part of Hot (set_control / the tick read and write it) */
@@ -740,16 +735,17 @@ SD bool tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     double acc_z = (h.w0 * (h.w2 * cx) + -(h.w1 * crx) * 2.0) + -(h.al1 * cx);
     double acc_x = cross_c(h.w1, -(h.w1 * cx), h.w2, h.w2 * cx) + (SETTLED ? 0.0 : h.coma);
     /* total force and linear acceleration (src/dynamics.py:5-10) */
+    /* F * (1/m) (product mode; src/dynamics.py:5-10 solves diag(m) a = F) */
     double na0, na1, na2;
-    const Rcp rm{m, g.rm};
+    const double rm = g.rm;
     if (RAND) {   /* + force noise (z: zero) */
-        na0 = qdiv(sm_mad(acc_x, m, (((jf0 + df0) + af0) + cf0) + nf0), rm);
-        na1 = qdiv(sm_mad(acc_y, m, (((jf1 + df1) + af1) + cf1) + nf1), rm);
-        na2 = qdiv(sm_mad(acc_z, m, (((jf2 + df2) + af2) + cf2) + 0.0), rm);
+        na0 = sm_mad(acc_x, m, (((jf0 + df0) + af0) + cf0) + nf0) * rm;
+        na1 = sm_mad(acc_y, m, (((jf1 + df1) + af1) + cf1) + nf1) * rm;
+        na2 = sm_mad(acc_z, m, (((jf2 + df2) + af2) + cf2) + 0.0) * rm;
     } else {
-        na0 = qdiv(sm_mad(acc_x, m, ((jf0 + df0) + af0) + cf0), rm);
-        na1 = qdiv(sm_mad(acc_y, m, ((jf1 + df1) + af1) + cf1), rm);
-        na2 = qdiv(sm_mad(acc_z, m, ((jf2 + df2) + af2) + cf2), rm);
+        na0 = sm_mad(acc_x, m, ((jf0 + df0) + af0) + cf0) * rm;
+        na1 = sm_mad(acc_y, m, ((jf1 + df1) + af1) + cf1) * rm;
+        na2 = sm_mad(acc_z, m, ((jf2 + df2) + af2) + cf2) * rm;
     }
     /* ---------------- Euler ---------------- */
     const double I0 = g.I0, I1 = g.I1;
@@ -781,16 +777,17 @@ SD bool tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     double amt1 = -(sm_mad(at1, h.al1, cross_c(h.w2, atw0, h.w0, atw2)) + cross_c(h.v2, amv0, h.v0, amv2));
     double amt2 = -(sm_mad(at2, h.al2, cross_c(h.w0, atw1, h.w1, atw0)) + cross_c(h.v0, amv1, h.v1, amv0));
     /* total torque and angular acceleration (src/dynamics.py:13-17) */
+    /* tau * (1/I) (product mode; src/dynamics.py:13-17) */
     double nal0, nal1, nal2;
-    const Rcp rI0{I0, g.rI0}, rI1{I1, g.rI1};
+    const double rI0 = g.rI0, rI1 = g.rI1;
     if (RAND) {   /* + torque noise (x, y: zero) */
-        nal0 = qdiv((sm_mad(-ir0, h.w0, dt0 + ct0) + amt0) + 0.0, rI0);
-        nal1 = qdiv((sm_mad(-ir1, h.w1, (jt1 + dt1) + ct1) + amt1) + 0.0, rI1);
-        nal2 = qdiv((sm_mad(-ir2, h.w2, (jt2 + dt2) + ct2) + amt2) + nt2, rI1);
+        nal0 = ((sm_mad(-ir0, h.w0, dt0 + ct0) + amt0) + 0.0) * rI0;
+        nal1 = ((sm_mad(-ir1, h.w1, (jt1 + dt1) + ct1) + amt1) + 0.0) * rI1;
+        nal2 = ((sm_mad(-ir2, h.w2, (jt2 + dt2) + ct2) + amt2) + nt2) * rI1;
     } else {
-        nal0 = qdiv(sm_mad(-ir0, h.w0, dt0 + ct0) + amt0, rI0);
-        nal1 = qdiv(sm_mad(-ir1, h.w1, (jt1 + dt1) + ct1) + amt1, rI1);
-        nal2 = qdiv(sm_mad(-ir2, h.w2, (jt2 + dt2) + ct2) + amt2, rI1);
+        nal0 = (sm_mad(-ir0, h.w0, dt0 + ct0) + amt0) * rI0;
+        nal1 = (sm_mad(-ir1, h.w1, (jt1 + dt1) + ct1) + amt1) * rI1;
+        nal2 = (sm_mad(-ir2, h.w2, (jt2 + dt2) + ct2) + amt2) * rI1;
     }
     if (REC) {
         const double z = 0.0;
@@ -814,12 +811,15 @@ SD bool tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     /* ---------------- integrate (semi-implicit Euler) ---------------- */
     h.v0 = sm_mad(na0, DT, h.v0); h.v1 = sm_mad(na1, DT, h.v1); h.v2 = sm_mad(na2, DT, h.v2);
     h.w0 = sm_mad(nal0, DT, h.w0); h.w1 = sm_mad(nal1, DT, h.w1); h.w2 = sm_mad(nal2, DT, h.w2);
-    {   /* to_euler_angle_rate_jit (src/dynamics.py:20-31) at the current angles */
-        const Rcp rc = rcp_of(h.cth);
-        double tt = qdiv(h.st, rc);
-        double r0 = sm_fma(h.cp * tt, h.w2, h.w0 + (h.sp * tt) * h.w1);
+    {   /* to_euler_angle_rate_jit (src/dynamics.py:20-31) at the current angles;
+         * product mode (the oracle's to_euler_angle_rate): u = sin(phi) w1 +
+         * cos(phi) w2, g = u / cos(theta) is row 2 and tan(theta) u = sin(theta) g
+         * row 0's tail */
+        const double u = sm_fma(h.cp, h.w2, h.sp * h.w1);
+        const double g2 = qdiv(u, rcp_of(h.cth));
+        double r0 = sm_fma(h.st, g2, h.w0);
         double r1 = sm_fma(-h.sp, h.w2, h.cp * h.w1);
-        double r2 = sm_fma(qdiv(h.cp, rc), h.w2, qdiv(h.sp, rc) * h.w1);
+        double r2 = g2;
         h.e0 = sm_mad(r0, DT, h.e0); h.e1 = sm_mad(r1, DT, h.e1); h.e2 = sm_mad(r2, DT, h.e2);
         if (REC) {
             rec[(int64_t)SALP_T_ETAR0 * rs] = r0;
@@ -827,14 +827,13 @@ SD bool tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
             rec[(int64_t)SALP_T_ETAR2 * rs] = r2;
         }
     }
-    {   /* to_world_frame_jit (src/dynamics.py:34-58) at the new angles */
+    {   /* to_world_frame_jit (src/dynamics.py:34-58) at the new angles (world_frame;
+         * roll / pitch sin / cos kept for the next tick's Euler-rate map) */
         double ss, cs;
-        sm_sincos_p(h.e0, &h.sp, &h.cp, P.sk);
-        sm_sincos_p(h.e1, &h.st, &h.cth, P.sk);
-        sm_sincos_nb_p(h.e2, &ss, &cs, P.sk);   /* yaw: both kinds of argument in a wave */
-        Rot R = rot_sc(h.sp, h.cp, h.st, h.cth, ss, cs);
+        sm_sincos_rp2(h.e0, h.e1, &h.sp, &h.cp, &h.st, &h.cth, P.sk);
+        sm_sincos_yaw_p(h.e2, &ss, &cs, P.sk);
         double vw[3];
-        rot_apply(R, h.v0, h.v1, h.v2, vw);
+        sm_world_frame(h.sp, h.cp, h.st, h.cth, ss, cs, h.v0, h.v1, h.v2, vw);
         h.p0 = sm_mad(vw[0], DT, h.p0); h.p1 = sm_mad(vw[1], DT, h.p1); h.p2 = sm_mad(vw[2], DT, h.p2);
     }
     h.q0 = sm_mad(h.v0, DT, h.q0); h.q1 = sm_mad(h.v1, DT, h.q1); h.q2 = sm_mad(h.v2, DT, h.q2);
@@ -1114,9 +1113,8 @@ SD void record_state(const Hot& h, const Params& P, ST S, int64_t i, double* rec
     put(SALP_T_RCD0, rcd_x(sh.nr)); put(SALP_T_RCD1, rcd_y(sh.nr)); put(SALP_T_RCD2, rcd_y(sh.nr));
     put(SALP_T_COM, h.com); put(SALP_T_COM_RATE, h.comr); put(SALP_T_COM_ACC, h.coma);
     /* get_front_position_world_frame (src/robot.py:924-928) */
-    const Rot R = rot_zyx(h.e0, h.e1, h.e2);
     double fw[3];
-    rot_apply(R, h.L / 2, 0.0, 0.0, fw);
+    world_frame(h.e0, h.e1, h.e2, h.L / 2, 0.0, 0.0, fw, sm_poly());
     put(SALP_T_FRONT_W0, fw[0]); put(SALP_T_FRONT_W1, fw[1]); put(SALP_T_FRONT_W2, fw[2]);
     if (first) {
         for (int k = SALP_T_FIRST_FORCE; k < SALP_TRACE_DIM; ++k) put(k, NAN);
@@ -1174,9 +1172,9 @@ template <bool RAND = false, class ST>
 SD StepOut finish_step(Hot& h, ST S, const Params& P, int64_t i, float* obs,
                        double* info) {
     StepOut out;
-    const Rot R = rot_zyx(h.e0, h.e1, h.e2);
+    const Rot R = rot_zyx(h.e0, h.e1, h.e2);   /* the body frame of the observation and the reward */
     double vw[3];
-    rot_apply(R, h.v0, h.v1, h.v2, vw);
+    world_frame(h.e0, h.e1, h.e2, h.v0, h.v1, h.v2, vw, sm_poly());
     const double px = h.p0, py = h.p1;
     /* episode_positions / episode_velocities */
     double path = SF(SALP_F_PATH_LEN) + np_norm2(px - SF(SALP_F_LAST_PX), py - SF(SALP_F_LAST_PY));

@@ -656,6 +656,34 @@ __device__ __forceinline__ bool unsteady(const Hot& h, const Params& P, bool act
     return active && h.ct < h.b2 && !salp::next_tick_steady(h, P);
 }
 
+// The env-step boundary of one lane of k_rollout (cold fields into registers,
+// the whole Hot from its LDS slot, rollout_boundary, back).  The randomised
+// kernels run it as a separate (non-inlined) function: inlined into
+// k_rollout<true, true> (salp_collect with randomisation), the compiler's
+// register allocation of round 5's build stored two LDS addresses in place of
+// the discharge coefficient's slot (tests/test_gpu_collect.py, rand case;
+// tools/debug_collect_rand.py); the call keeps the boundary's registers apart
+// from the tick loop's.  The plain kernels keep it inline (the bench path).
+template <bool RAND, bool POL>
+__device__ __forceinline__ bool lane_boundary(const RolloutArgs& a, salp::SpillSlot sp, int64_t i, bool& pending,
+                                              bool& active, int64_t& steps, double* c32p) {
+    const uint64_t env_id = (uint64_t)(a.P.env_offset + i);
+    salp::ColdRegs<RAND> C;
+    salp::load_cold<RAND>(C, a.S, a.P, i);
+    Hot hb;
+    salp::unspill<RAND>(hb, sp, a.P, env_id);
+    rollout_boundary<RAND, POL>(hb, &C, a.P, i, env_id, pending, active, steps, a.max_steps, a.B,
+                                a.reward_sum, a.R, salp::Cache32{c32p});
+    salp::store_cold<RAND>(C, a.S, a.P, i);
+    salp::spill<RAND>(hb, sp);
+    return unsteady(hb, a.P, active);
+}
+template <bool RAND, bool POL>
+__device__ __noinline__ bool lane_boundary_call(const RolloutArgs* a, double* spp, int64_t i, bool* pending,
+                                                bool* active, int64_t* steps, double* c32p) {
+    return lane_boundary<RAND, POL>(*a, salp::SpillSlot{spp}, i, *pending, *active, *steps, c32p);
+}
+
 #if SALP_ROLLOUT_RESEAT
 template <bool RAND, bool POL>
 __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
@@ -694,17 +722,12 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
         bool uns = unsteady(h, P, active);
         salp::spill<RAND>(h, sp);
         if (need) {
-            const RolloutArgs a = fresh_args();
-            const uint64_t env_id = (uint64_t)(a.P.env_offset + i);
-            salp::ColdRegs<RAND> C;
-            salp::load_cold<RAND>(C, a.S, a.P, i);
-            Hot hb;
-            salp::unspill<RAND>(hb, sp, a.P, env_id);
-            rollout_boundary<RAND, POL>(hb, &C, a.P, i, env_id, pending, active, steps, a.max_steps, a.B,
-                                        a.reward_sum, a.R, salp::Cache32{s_cache32 + s});
-            salp::store_cold<RAND>(C, a.S, a.P, i);
-            salp::spill<RAND>(hb, sp);
-            uns = unsteady(hb, a.P, active);
+            if (RAND) {
+                uns = lane_boundary_call<RAND, POL>(&A, s_spill + s, i, &pending, &active, &steps, s_cache32 + s);
+            } else {
+                const RolloutArgs a = fresh_args();
+                uns = lane_boundary<RAND, POL>(a, sp, i, pending, active, steps, s_cache32 + s);
+            }
         }
         if (last) {
             const RolloutArgs a = fresh_args();
@@ -1430,6 +1453,20 @@ __global__ void k_math_selftest(const double* x, const double* y, int64_t n, dou
     out[9 * n + i] = snb;
     out[10 * n + i] = cnb;
     out[11 * n + i] = salp::qdiv(x[i], salp::rcp_of(y[i]));   /* the tick's shared-reciprocal division */
+    double sy, cy, s0, c0, s1, c1, sz, cz, wf[3];
+    sm_sincos_yaw_p(x[i], &sy, &cy, sm_poly());
+    out[12 * n + i] = sy;
+    out[13 * n + i] = cy;
+    sm_sincos_rp2(x[i], y[i], &s0, &c0, &s1, &c1, sm_poly());
+    out[14 * n + i] = s0;
+    out[15 * n + i] = c0;
+    out[16 * n + i] = s1;
+    out[17 * n + i] = c1;
+    sm_sincos_yaw_p(x[i] + y[i], &sz, &cz, sm_poly());
+    sm_world_frame(s0, c0, s1, c1, sz, cz, y[i], x[i], 1.0, wf);
+    out[18 * n + i] = wf[0];
+    out[19 * n + i] = wf[1];
+    out[20 * n + i] = wf[2];
 }
 
 const char* const kFieldNames[SALP_NUM_FIELDS] = {

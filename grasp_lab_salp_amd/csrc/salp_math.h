@@ -279,6 +279,95 @@ SM_QUAL void sm_sincos_nb_p(double x, double* s_out, double* c_out, SmPoly K) {
     *c_out = ((q + 1) & 2) ? -b : b;
 }
 SM_QUAL void sm_sincos(double x, double* s_out, double* c_out) { sm_sincos_p(x, s_out, c_out, sm_poly()); }
+
+/* ------------------------- the tick's sin/cos (round 5, SALP_FMA = 1) */
+/* The physics tick takes sin and cos of the three Euler angles every tick
+ * (src/dynamics.py:20-58): 21 % of k_rollout's executed instructions
+ * (profiles/r5a_ablation.json).  In the product mode (SALP_FMA = 1) the tick,
+ * the world-frame rotation and the Euler-rate map use the two functions below
+ * on both sides (device and oracle include this header), so the device still
+ * equals the oracle bit for bit; SALP_FMA = 0 keeps fdlibm's sm_sincos_p for
+ * every angle.  Both are within one ulp of sin / cos (tests/test_math.py), so
+ * the oracle stays inside the golden tolerances against the reference's own
+ * NumPy (glibc) sin / cos (tests/test_oracle_golden.py). */
+
+/* Roll and pitch stay small (|x| < 1/16 for 99.996 % of the ticks of a
+ * random-action run; oracle, 4 096 envs x 120 env-steps): there fdlibm's
+ * degree-13 / 14 kernels need only their first four terms (the dropped
+ * S5 x^11 and C5 x^12 are below 2^-60 relative).  sin x = x + x^3 (S1 + z S2
+ * + z^2 S3 + z^3 S4), cos x = w + (((1 - w) - z/2) + z r) with w = 1 - z/2 and
+ * r = z (C1 + z C2 + z^2 C3 + z^3 C4), z = x^2 (fdlibm's own cos form). */
+#define SM_SHORT_MAX 0.0625
+SM_QUAL void sm_sincos_short_p(double x, double* s_out, double* c_out, SmPoly K) {
+    const double z = x * x;
+    *s_out = sm_mad(z * x, sm_mad(z, sm_mad(z, sm_mad(z, K.S4, K.S3), K.S2), K.S1), x);
+    const double r = z * sm_mad(z, sm_mad(z, sm_mad(z, K.C4, K.C3), K.C2), K.C1);
+    const double hz = 0.5 * z, w = 1.0 - hz;
+    *c_out = w + sm_mad(z, r, (1.0 - w) - hz);
+}
+/* sin / cos of roll x0 and pitch x1 together: the short kernels for both when
+ * neither |x| exceeds 1/16 (NaN included: the kernels return NaN for it, and a
+ * diverged env's NaN angles do not send its wave down the long path), else
+ * fdlibm's sm_sincos_p for both.  The choice is a function of (x0, x1) alone
+ * (per lane, not per wave), so results do not depend on the other lanes. */
+SM_QUAL void sm_sincos_rp2(double x0, double x1, double* s0, double* c0, double* s1, double* c1, SmPoly K) {
+#if SALP_FMA
+    if (!(fabs(x0) > SM_SHORT_MAX || fabs(x1) > SM_SHORT_MAX)) {
+        sm_sincos_short_p(x0, s0, c0, K);
+        sm_sincos_short_p(x1, s1, c1, K);
+        return;
+    }
+#endif
+    sm_sincos_p(x0, s0, c0, K);
+    sm_sincos_p(x1, s1, c1, K);
+}
+/* sin / cos of the yaw (any size: the heading is uniform over the circle).
+ * fdlibm's reduction and kernels, streamlined for a SIMD lane (every step is
+ * branch-free):
+ *  - fn = rint(x 2/pi) and the quadrant come from one add of 1.5 * 2^52:
+ *    fn is in the low bits of x 2/pi + 1.5 * 2^52 (exact for |fn| < 2^51);
+ *  - one Cody-Waite stage (pio2_1, pio2_1t).  fdlibm adds a second and third
+ *    stage when more than 16 bits cancel (x within |x| 2^-16 of a multiple of
+ *    pi/2); the first stage's absolute error is below |fn| 1e-26, so the
+ *    result stays within one ulp unless |y| < |fn| 1e-10, and within 1e-26
+ *    absolute always;
+ *  - the tail forms of the kernels for every argument (y1 = 0 when fn = 0);
+ *  - quadrant swap as selects, the two signs as bit flips.
+ * Differs from sm_sincos_p by at most an ulp. */
+SM_QUAL void sm_sincos_yaw_p(double x, double* s_out, double* c_out, SmPoly K) {
+#if SALP_FMA
+    const double magic = 0x1.8p52;
+    const double t = x * K.R_INV + magic;
+    const double fn = t - magic;
+    const uint32_t q = (uint32_t)sm_d2u(t) & 3u;
+    const double r = sm_mad(-fn, K.R_P1, x);   /* fn * pio2_1 is exact (33-bit pio2_1) */
+    const double w = fn * K.R_P1T;
+    const double y0 = r - w;
+    const double y1 = (r - y0) - w;
+    const double z = y0 * y0, zz = z * z;
+    const double s = sm_ksin_tail(y0, y1, z, z * y0, sm_ksin_r(z, zz, K), K);
+    const double c = sm_kcos_p(y0, y1, K);
+    const double a = (q & 1u) ? c : s, b = (q & 1u) ? s : c;
+    *s_out = sm_u2d(sm_d2u(a) ^ ((uint64_t)(q & 2u) << 62));
+    *c_out = sm_u2d(sm_d2u(b) ^ ((uint64_t)((q + 1u) & 2u) << 62));
+#else
+    sm_sincos_p(x, s_out, c_out, K);
+#endif
+}
+
+/* R v for R = Rz(psi) Ry(theta) Rx(phi) (src/dynamics.py:34-58), given the
+ * sin / cos of the three angles.  SALP_FMA = 1: the three plane rotations
+ * applied in turn, Rz (Ry (Rx v)), 12 operations, each component one product
+ * fused into a sum; the same vector up to rounding as NumPy's (R_z @ R_y @
+ * R_x) @ v, which builds the matrix first (the oracle's SALP_FMA = 0 path). */
+SM_QUAL void sm_world_frame(double sp, double cp, double st, double ct, double ss, double cs, double v0,
+                            double v1, double v2, double* o) {
+    const double x1 = sm_fma(cp, v1, -(sp * v2)), x2 = sm_fma(sp, v1, cp * v2);   /* Rx v */
+    const double y0 = sm_fma(ct, v0, st * x2), y2 = sm_fma(-st, v0, ct * x2);     /* Ry (Rx v) */
+    o[0] = sm_fma(cs, y0, -(ss * x1));                                          /* Rz (Ry (Rx v)) */
+    o[1] = sm_fma(ss, y0, cs * x1);
+    o[2] = y2;
+}
 SM_QUAL double sm_sin(double x) { double s, c; sm_sincos(x, &s, &c); return s; }
 SM_QUAL double sm_cos(double x) { double s, c; sm_sincos(x, &s, &c); return c; }
 SM_QUAL double sm_tan(double x) { double s, c; sm_sincos(x, &s, &c); return s / c; }

@@ -107,9 +107,8 @@ SD void pair_clock(double& ct, int& phase, double b1, double b2, double mx) {
  * to_world_frame_jit block): yaw sin/cos, R at the new angles (roll / pitch
  * sin/cos from wave B), p += (R v) dt. */
 SD void a_world(HotA& h, const Params&) {
-    const Rot R = rot_sc(h.sp, h.cp, h.st, h.cth, h.ss, h.cs);
     double vw[3];
-    rot_apply(R, h.v0, h.v1, h.v2, vw);
+    sm_world_frame(h.sp, h.cp, h.st, h.cth, h.ss, h.cs, h.v0, h.v1, h.v2, vw);
     h.p0 = sm_mad(vw[0], DT, h.p0); h.p1 = sm_mad(vw[1], DT, h.p1); h.p2 = sm_mad(vw[2], DT, h.p2);
 }
 
@@ -121,9 +120,8 @@ SD void a_world(HotA& h, const Params&) {
  * world-frame update (yaw sin/cos, R v), this tick's clock / phase / mass-side
  * geometry and Newton's equations (the geometry into temporaries, committed
  * after Newton, which reads the tick-start values); wave B its shape-side
- * geometry with Euler's equations, and both roll / pitch sin/cos on one
- * straight path when every ticking lane's angles are small, then the yaw's
- * for wave A.  Every value is the expression tick() computes. */
+ * geometry with Euler's equations, roll / pitch sin/cos (salp_math.h
+ * sm_sincos_rp2), then the yaw's for wave A.  Every value is the expression tick() computes. */
 
 /* A tick's clock, phase and (full ticks) mass-side geometry: a function of
  * wave A's own state alone.  (Computing it between publishing and waiting,
@@ -159,7 +157,7 @@ SD PreA pre_a(const HotA& h, const Params& P, Cache32 c32) {
         jet_rates(P, V, h.V, wm, f, h.g32, ng);   /* pV <- V, pv32 <- g32 first (tick()) */
         mr = ng.mr;
         sp = ng.speed;
-        rmn = rcp_of(mn).r;
+        rmn = rcr(mn);
     }
     return PreA{ct, L, W, V, com, comr, coma, mn, mr, sp, rmn, phase, f};
 }
@@ -172,9 +170,8 @@ SD bool step_a_newton(HotA& h, const Params& P, const PreA& g);
 template <int MODE>
 SD bool step_a(HotA& h, const Params& P, const PreA& g, bool pend) {
     {   /* a_world of the previous tick, with v before this tick's Newton */
-        const Rot R = rot_sc(h.sp, h.cp, h.st, h.cth, h.ss, h.cs);
         double vw[3];
-        rot_apply(R, h.v0, h.v1, h.v2, vw);
+        sm_world_frame(h.sp, h.cp, h.st, h.cth, h.ss, h.cs, h.v0, h.v1, h.v2, vw);
         const double p0 = sm_mad(vw[0], DT, h.p0), p1 = sm_mad(vw[1], DT, h.p1), p2 = sm_mad(vw[2], DT, h.p2);
         h.p0 = pend ? p0 : h.p0;
         h.p1 = pend ? p1 : h.p1;
@@ -205,10 +202,10 @@ SD bool step_a_newton(HotA& h, const Params& P, const PreA& g) {
     double acc_y = (h.w0 * (h.w1 * cx) + (h.w2 * crx) * 2.0) + h.al2 * cx;
     double acc_z = (h.w0 * (h.w2 * cx) + -(h.w1 * crx) * 2.0) + -(h.al1 * cx);
     double acc_x = cross_c(h.w1, -(h.w1 * cx), h.w2, h.w2 * cx) + (SETTLED ? 0.0 : h.coma);
-    const Rcp rm{m, h.rm};
-    const double na0 = qdiv(sm_mad(acc_x, m, ((h.jf0 + df0) + af0) + cf0), rm);
-    const double na1 = qdiv(sm_mad(acc_y, m, ((h.jf1 + df1) + af1) + cf1), rm);
-    const double na2 = qdiv(sm_mad(acc_z, m, ((h.jf2 + df2) + af2) + cf2), rm);
+    const double rm = h.rm;
+    const double na0 = sm_mad(acc_x, m, ((h.jf0 + df0) + af0) + cf0) * rm;
+    const double na1 = sm_mad(acc_y, m, ((h.jf1 + df1) + af1) + cf1) * rm;
+    const double na2 = sm_mad(acc_z, m, ((h.jf2 + df2) + af2) + cf2) * rm;
     h.a0 = na0; h.a1 = na1; h.a2 = na2;
     h.v0 = sm_mad(na0, DT, h.v0); h.v1 = sm_mad(na1, DT, h.v1); h.v2 = sm_mad(na2, DT, h.v2);
     h.q0 = sm_mad(h.v0, DT, h.q0); h.q1 = sm_mad(h.v1, DT, h.q1); h.q2 = sm_mad(h.v2, DT, h.q2);
@@ -270,8 +267,8 @@ SD PreB pre_b(const HotB& h, const Params& P, Cache32 c32) {
             ng.kc0 = c32[C32_KC0]; ng.kc1 = c32[C32_KC1]; ng.ra0 = c32[C32_RA0]; ng.ra1 = c32[C32_RA1];
             ng.dimx = c32[C32_DIMX]; ng.dimy = c32[C32_DIMY];
         }
-        ng.rI0 = rcp_of(ng.I0).r;
-        ng.rI1 = rcp_of(ng.I1).r;
+        ng.rI0 = rcr(ng.I0);
+        ng.rI1 = rcr(ng.I1);
     }
     return PreB{ct, L, W, ng, phase, f};
 }
@@ -302,10 +299,10 @@ SD void step_b1(HotB& h, const Params& P) {
     double amt0 = -(sm_mad(at0, h.al0, cross_c(h.w1, atw2, h.w2, atw1)) + h.X0);
     double amt1 = -(sm_mad(at1, h.al1, cross_c(h.w2, atw0, h.w0, atw2)) + h.X1);
     double amt2 = -(sm_mad(at2, h.al2, cross_c(h.w0, atw1, h.w1, atw0)) + h.X2);
-    const Rcp rI0{I0, h.rI0}, rI1{I1, h.rI1};
-    const double nal0 = qdiv(sm_mad(-ir0, h.w0, dt0 + ct0) + amt0, rI0);
-    const double nal1 = qdiv(sm_mad(-ir1, h.w1, (h.jt1 + dt1) + ct1) + amt1, rI1);
-    const double nal2 = qdiv(sm_mad(-ir2, h.w2, (h.jt2 + dt2) + ct2) + amt2, rI1);
+    const double rI0 = h.rI0, rI1 = h.rI1;
+    const double nal0 = (sm_mad(-ir0, h.w0, dt0 + ct0) + amt0) * rI0;
+    const double nal1 = (sm_mad(-ir1, h.w1, (h.jt1 + dt1) + ct1) + amt1) * rI1;
+    const double nal2 = (sm_mad(-ir2, h.w2, (h.jt2 + dt2) + ct2) + amt2) * rI1;
     h.al0 = nal0; h.al1 = nal1; h.al2 = nal2;
     h.w0 = sm_mad(nal0, DT, h.w0); h.w1 = sm_mad(nal1, DT, h.w1); h.w2 = sm_mad(nal2, DT, h.w2);
 }
@@ -315,12 +312,12 @@ SD void step_b1(HotB& h, const Params& P) {
 template <int MODE>
 SD void step_b2(HotB& h, const Params& P, const PreB& g) {
     constexpr bool STEADY = MODE != PM_FULL;
-    {
-        const Rcp rc = rcp_of(h.cth);
-        double tt = qdiv(h.st, rc);
-        double r0 = sm_fma(h.cp * tt, h.w2, h.w0 + (h.sp * tt) * h.w1);
+    {   /* tick()'s Euler-rate map */
+        const double u = sm_fma(h.cp, h.w2, h.sp * h.w1);
+        const double g2 = qdiv(u, rcp_of(h.cth));
+        double r0 = sm_fma(h.st, g2, h.w0);
         double r1 = sm_fma(-h.sp, h.w2, h.cp * h.w1);
-        double r2 = sm_fma(qdiv(h.cp, rc), h.w2, qdiv(h.sp, rc) * h.w1);
+        double r2 = g2;
         h.e0 = sm_mad(r0, DT, h.e0); h.e1 = sm_mad(r1, DT, h.e1); h.e2 = sm_mad(r2, DT, h.e2);
     }
     h.g0 = sm_mad(h.w0, DT, h.g0); h.g1 = sm_mad(h.w1, DT, h.g1); h.g2 = sm_mad(h.w2, DT, h.g2);
@@ -332,8 +329,8 @@ SD void step_b2(HotB& h, const Params& P, const PreB& g) {
         h.kc0 = g.ng.kc0; h.kc1 = g.ng.kc1; h.ra0 = g.ng.ra0; h.ra1 = g.ng.ra1;
         h.dimx = g.ng.dimx; h.dimy = g.ng.dimy;
     }
-    sincos2_p(h.e0, h.e1, &h.sp, &h.cp, &h.st, &h.cth, P.sk);
-    sm_sincos_nb_p(h.e2, &h.ss, &h.cs, P.sk);   /* yaw: wave A's world-frame update */
+    sm_sincos_rp2(h.e0, h.e1, &h.sp, &h.cp, &h.st, &h.cth, P.sk);
+    sm_sincos_yaw_p(h.e2, &h.ss, &h.cs, P.sk);   /* yaw: wave A's world-frame update */
 }
 template <int MODE>
 SD void step_b(HotB& h, const Params& P, const PreB& g) {
@@ -402,7 +399,7 @@ SD void unspill_a(HotA& h, SpillSlot s) {
     const int fl = (int)s[SP_FLAGS];
     h.phase = fl & 3; h.g32 = (fl & 4) != 0; h.pv32 = (fl & 8) != 0; h.c32 = (fl & 16) != 0;
     h.m = s[SP_M]; h.mr = s[SP_MR]; h.speed = s[SP_SPEED];
-    h.rm = rcp_of(h.m).r;
+    h.rm = rcr(h.m);
     /* wave B's state, as its packet would carry it */
     h.w0 = s[SP_W]; h.w1 = s[SP_W + 1]; h.w2 = s[SP_W + 2];
     h.al1 = s[SP_AL + 1]; h.al2 = s[SP_AL + 2];
@@ -420,11 +417,11 @@ SD void unspill_b(HotB& h, SpillSlot s, const Params& P) {
     h.g0 = s[SP_G]; h.g1 = s[SP_G + 1]; h.g2 = s[SP_G + 2];
     h.pI0 = s[SP_PI]; h.pI1 = s[SP_PI + 1]; h.pI2 = s[SP_PI + 2];
     h.sp = s[SP_SP]; h.cp = s[SP_CP]; h.st = s[SP_ST]; h.cth = s[SP_CTH];
-    sm_sincos_nb_p(h.e2, &h.ss, &h.cs, P.sk);
+    sm_sincos_yaw_p(h.e2, &h.ss, &h.cs, P.sk);
     h.I0 = s[SP_I0]; h.I1 = s[SP_I1]; h.kc0 = s[SP_KC0]; h.kc1 = s[SP_KC1];
     h.ra0 = s[SP_RA0]; h.ra1 = s[SP_RA1]; h.dimx = s[SP_DIMX]; h.dimy = s[SP_DIMY];
-    h.rI0 = rcp_of(h.I0).r;
-    h.rI1 = rcp_of(h.I1).r;
+    h.rI0 = rcr(h.I0);
+    h.rI1 = rcr(h.I1);
     h.L = s[SP_L]; h.W = s[SP_WID]; h.ct = s[SP_CT];
     h.refill = s[SP_REFILL]; h.c = s[SP_C]; h.cr = s[SP_CR]; h.rr = s[SP_RR];
     const double jet = s[SP_JET], coast = s[SP_COAST], turn = s[SP_TURN];

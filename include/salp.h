@@ -433,9 +433,14 @@ int salp_bench_ticks(SalpEnv* h, int32_t n_ticks, void* stream);
  * boundaries touch, grasp_lab_salp_amd/csrc/salp_device.h "state layout");
  * use salp_get_state / salp_set_state for the field-major view. */
 int64_t salp_state_ptr(SalpEnv* h);
-/* Device-side self-test of salp_math.h: out[i] = f(x[i]) for f in
- * {sin, cos, tan, atan2(x, y), asin, acos, cube, np_cosf, np_sinf, sin and cos
- * of the branch-free sincos}.  x, y [n]; out [11][n]. */
+/* Device-side self-test of salp_math.h: out[r * n + i] for the rows
+ * {0 sin, 1 cos, 2 tan, 3 atan2(x, y), 4 asin, 5 acos, 6 cube, 7 np_cosf,
+ * 8 np_sinf, 9-10 sin and cos of the branch-free sincos, 11 x / y by the
+ * tick's shared-reciprocal division, 12-13 sin and cos of the tick's yaw
+ * function, 14-17 sin x, cos x, sin y, cos y of the tick's roll / pitch pair
+ * function at (x, y), 18-20 the tick's world-frame rotation of (y, x, 1) by
+ * the angles (x, y, x + y)}, x, y [n]; out [SALP_MATH_SELFTEST_ROWS][n]. */
+#define SALP_MATH_SELFTEST_ROWS 21
 int salp_math_selftest(const double* x, const double* y, int64_t n, double* out, void* stream);
 
 /* State fields.  Names follow the reference attribute they hold. */

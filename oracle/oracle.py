@@ -10,7 +10,7 @@ import subprocess
 
 import numpy as np
 
-from grasp_lab_salp_amd._abi import (INFO_DIM, MAX_OBSTACLES, NUM_FIELDS, OBS_DIM_MAX,
+from grasp_lab_salp_amd._abi import (INFO_DIM, MATH_SELFTEST_ROWS, MAX_OBSTACLES, NUM_FIELDS, OBS_DIM_MAX,
                                      TRACE_DIM, SalpParams, default_params)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -55,7 +55,7 @@ def lib(exact=False):
                                          ctypes.c_int]
         L.oracle_step_random.restype = i64
         L.oracle_replay.argtypes = [sp, i64, P(i64), P(i64), P(d), ctypes.c_uint64, P(d), i64, P(f), P(f),
-                                    P(f), P(f), P(u8), ctypes.c_int, ctypes.c_int]
+                                    P(f), P(f), P(u8), ctypes.c_int, ctypes.c_int, P(i64)]
         L.oracle_replay.restype = i64
         L.oracle_robot_trace.argtypes = [sp, P(f), ctypes.c_int, P(d), i64]
         L.oracle_robot_trace.restype = i64
@@ -199,12 +199,16 @@ class Oracle:
         return rs, int(ticks)
 
 
-def replay(env_ids, n_steps, ct_stop=None, seed=0, params=None, capacity=0, threads=0, exact=False):
+def replay(env_ids, n_steps, ct_stop=None, seed=0, params=None, capacity=0, threads=0, exact=False,
+           ticks_out=None):
     """Sampled envs of a chained random-action rollout (oracle_replay): env j,
     global id env_ids[j], from creation through n_steps[j] env-steps, then the
     in-flight cycle up to cycle_time ct_stop[j] (< 0: none).  Returns (state
     [NUM_FIELDS, n], buffers {obs, obs_before, actions, rewards, dones} with
-    `capacity` slots (slot = step % capacity, the last `capacity` steps)."""
+    `capacity` slots (slot = step % capacity, the last `capacity` steps).
+    ticks_out (int64 [n], optional) receives the physics ticks of each env's
+    n_steps[j] completed env-steps (src/robot.py:756-757 loop iterations; the
+    in-flight cycle is not counted)."""
     params = params if params is not None else default_params()
     ids = np.ascontiguousarray(env_ids, np.int64)
     n = len(ids)
@@ -222,7 +226,8 @@ def replay(env_ids, n_steps, ct_stop=None, seed=0, params=None, capacity=0, thre
                         _p(ct, ctypes.c_double), int(seed), _p(state, ctypes.c_double), cap,
                         _p(b["obs"], ctypes.c_float), _p(b["obs_before"], ctypes.c_float),
                         _p(b["actions"], ctypes.c_float), _p(b["rewards"], ctypes.c_float),
-                        _p(b["dones"], ctypes.c_uint8), od, int(threads))
+                        _p(b["dones"], ctypes.c_uint8), od, int(threads),
+                        None if ticks_out is None else _p(ticks_out, ctypes.c_int64))
     return state, (b if cap > 0 else None)
 
 
@@ -240,7 +245,7 @@ def robot_trace(actions, params=None, max_rows=200000, exact=False):
 def math_selftest(x, y, exact=False):
     x = np.ascontiguousarray(x, np.float64)
     y = np.ascontiguousarray(y, np.float64)
-    out = np.zeros((12, len(x)), np.float64)
+    out = np.zeros((MATH_SELFTEST_ROWS, len(x)), np.float64)
     lib(exact).oracle_math_selftest(_p(x, ctypes.c_double), _p(y, ctypes.c_double), len(x),
                                _p(out, ctypes.c_double))
     return out

@@ -558,6 +558,17 @@ static V3 compute_added_mass_torque(M3 I, M3 amct, M3 I_rate, M3 amrct, M3 mass,
 /* src/dynamics.py:20-31 */
 static V3 to_euler_angle_rate(V3 eta, V3 w) {
     double sp, cp, st, ct;
+#if SALP_FMA
+    /* product mode (salp_math.h, round 5): the tick's roll / pitch sin / cos,
+     * and T @ w regrouped: u = sin(phi) w1 + cos(phi) w2 is both row 2 times
+     * cos(theta) and, times tan(theta), row 0's tail, so one division
+     * g = u / cos(theta) serves rows 0 and 2 (the device computes the same
+     * expressions) */
+    sm_sincos_rp2(eta.v[0], eta.v[1], &sp, &cp, &st, &ct, sm_poly());
+    const double u = sm_fma(cp, w.v[2], sp * w.v[1]);
+    const double g = u / ct;
+    return v3(sm_fma(st, g, w.v[0]), sm_fma(-sp, w.v[2], cp * w.v[1]), g);
+#endif
     sm_sincos(eta.v[0], &sp, &cp);
     sm_sincos(eta.v[1], &st, &ct);
     double tt = sm_tan(eta.v[1]);
@@ -579,7 +590,20 @@ static M3 rot_zyx(V3 eta) {
     Rz.m[0][0] = cs; Rz.m[0][1] = -ss; Rz.m[1][0] = ss; Rz.m[1][1] = cs; Rz.m[2][2] = 1.0;
     return mmul(mmul(Rz, Ry), Rx);
 }
-static V3 to_world_frame(V3 eta, V3 x) { return mvec(rot_zyx(eta), x); }
+static V3 to_world_frame(V3 eta, V3 x) {
+#if SALP_FMA
+    /* product mode (salp_math.h, round 5): the tick's sin / cos and the three
+     * plane rotations in turn, as the device's tick, finish_step and trace */
+    double sp, cp, st, ct, ss, cs;
+    sm_sincos_rp2(eta.v[0], eta.v[1], &sp, &cp, &st, &ct, sm_poly());
+    sm_sincos_yaw_p(eta.v[2], &ss, &cs, sm_poly());
+    V3 r;
+    sm_world_frame(sp, cp, st, ct, ss, cs, x.v[0], x.v[1], x.v[2], r.v);
+    return r;
+#else
+    return mvec(rot_zyx(eta), x);
+#endif
+}
 static V3 to_body_frame(V3 eta, V3 x) { return mTvec(rot_zyx(eta), x); }
 
 /* --------------------------------------------------------- Robot methods */
@@ -758,8 +782,14 @@ static V3 robot_newton(Obj* o) {
     V3 total = vmad(a_sum, o->mass.m[0][0],
                     vadd(vadd(vadd(vadd(o->jet_force, o->drag_force), o->added_mass_force), o->coriolis_force),
                          noise));
-    /* np.linalg.solve(diag(m), F) == F / m (probed) */
+    /* np.linalg.solve(diag(m), F) == F / m (probed); product mode: F times
+     * the correctly rounded 1 / m (the device keeps 1 / m with the geometry) */
+#if SALP_FMA
+    return v3(total.v[0] * (1.0 / o->mass.m[0][0]), total.v[1] * (1.0 / o->mass.m[1][1]),
+              total.v[2] * (1.0 / o->mass.m[2][2]));
+#else
     return v3(total.v[0] / o->mass.m[0][0], total.v[1] / o->mass.m[1][1], total.v[2] / o->mass.m[2][2]);
+#endif
 }
 /* src/robot.py:825-851 */
 static V3 robot_euler(Obj* o) {
@@ -784,7 +814,12 @@ static V3 robot_euler(Obj* o) {
     part = vadd(part, o->deform_torque);
 #endif
     V3 total = vadd(vadd(part, o->added_mass_torque), noise);
+#if SALP_FMA
+    /* product mode: times the correctly rounded 1 / I (as robot_newton) */
+    return v3(total.v[0] * (1.0 / I.m[0][0]), total.v[1] * (1.0 / I.m[1][1]), total.v[2] * (1.0 / I.m[2][2]));
+#else
     return v3(total.v[0] / I.m[0][0], total.v[1] / I.m[1][1], total.v[2] / I.m[2][2]);
+#endif
 }
 /* src/robot.py:860-875 */
 static void robot_update_motion_states(Obj* o) {
@@ -1410,7 +1445,7 @@ int64_t oracle_step_random(const SalpParams* p, int64_t n, double* state, int32_
 int64_t oracle_replay(const SalpParams* p, int64_t n, const int64_t* env_ids, const int64_t* n_steps,
                       const double* ct_stop, uint64_t seed, double* state, int64_t cap, float* obs,
                       float* obs_before, float* actions, float* rewards, uint8_t* dones, int obs_dim,
-                      int nthreads) {
+                      int nthreads, int64_t* ticks_out) {
     int64_t total_ticks = 0;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
@@ -1431,6 +1466,7 @@ int64_t oracle_replay(const SalpParams* p, int64_t n, const int64_t* env_ids, co
         int nob;
         env_draw_reset(&o, seed, id, tgt, obst, &nob);
         env_reset_with(&o, tgt, obst, nob, cur);
+        int64_t done_ticks = 0;   /* ticks of the completed env-steps (in-flight cycle excluded) */
         for (int64_t k = 0; k < n_steps[j]; ++k) {
             float a[3], ob[SALP_OBS_DIM_MAX];
             uint8_t te, tr;
@@ -1438,7 +1474,7 @@ int64_t oracle_replay(const SalpParams* p, int64_t n, const int64_t* env_ids, co
             const int rec = cap > 0 && k >= n_steps[j] - cap;
             const size_t row = (size_t)(k % (cap > 0 ? cap : 1)) * (size_t)n + (size_t)j;
             if (rec && obs_before) memcpy(obs_before + row * obs_dim, cur, sizeof(float) * obs_dim);
-            total_ticks += env_begin_and_run_cycle(&o, a);
+            done_ticks += env_begin_and_run_cycle(&o, a);
             o.step_count += 1.0;
             double rw = env_finish_step(&o, ob, &te, &tr, NULL);
             if (rec) {
@@ -1453,6 +1489,8 @@ int64_t oracle_replay(const SalpParams* p, int64_t n, const int64_t* env_ids, co
             }
             memcpy(cur, ob, sizeof(float) * obs_dim);
         }
+        total_ticks += done_ticks;
+        if (ticks_out) ticks_out[j] = done_ticks;
         if (ct_stop && ct_stop[j] >= 0.0) {
             float a[3];
             sp_action(seed, id, (uint64_t)o.step_count, a);
@@ -1597,6 +1635,20 @@ void oracle_math_selftest(const double* x, const double* y, int64_t n, double* o
         out[9 * n + i] = snb;
         out[10 * n + i] = cnb;
         out[11 * n + i] = x[i] / y[i];   /* device: qdiv(x, rcp_of(y)) */
+        double sy, cy, s0, c0, s1, c1, sz, cz, wf[3];
+        sm_sincos_yaw_p(x[i], &sy, &cy, sm_poly());
+        out[12 * n + i] = sy;
+        out[13 * n + i] = cy;
+        sm_sincos_rp2(x[i], y[i], &s0, &c0, &s1, &c1, sm_poly());
+        out[14 * n + i] = s0;
+        out[15 * n + i] = c0;
+        out[16 * n + i] = s1;
+        out[17 * n + i] = c1;
+        sm_sincos_yaw_p(x[i] + y[i], &sz, &cz, sm_poly());
+        sm_world_frame(s0, c0, s1, c1, sz, cz, y[i], x[i], 1.0, wf);
+        out[18 * n + i] = wf[0];
+        out[19 * n + i] = wf[1];
+        out[20 * n + i] = wf[2];
     }
 }
 

@@ -76,8 +76,9 @@ def check(state, steps_done, buffers, params, seed, env_offset=0, ids=None, thre
     pending = state[FIELD["pending"], ids] != 0.0
     ct = np.where(pending, state[FIELD["cycle_time"], ids], -1.0)
     cap = 0 if buffers is None else int(buffers["dones"].shape[0])
+    ticks = np.zeros(len(ids), np.int64)
     o_state, o_buf = orc.replay(ids + env_offset, k, ct, seed=seed, params=params, capacity=cap,
-                                threads=threads or _threads())
+                                threads=threads or _threads(), ticks_out=ticks)
     d = _bits_differ(state[:, ids], o_state)
     signed_zero = int((_bits_differ(state[:, ids], o_state, zeros=False) & ~d).sum())
     bad_fields = {}
@@ -97,7 +98,11 @@ def check(state, steps_done, buffers, params, seed, env_offset=0, ids=None, thre
            "env_steps_replayed": int(k.sum()), "steps_done_min": int(k.min()), "steps_done_max": int(k.max()),
            "pending_checked": int(pending.sum()), "state_mismatch_envs": int(env_bad.sum()),
            "state_mismatch_fields": bad_fields, "examples": examples,
-           "signed_zero_only_values": signed_zero}
+           "signed_zero_only_values": signed_zero,
+           # the physics ticks (src/robot.py:756-757 iterations) of the replayed
+           # completed env-steps: the measured mean cycle length of this run
+           "ticks_replayed": int(ticks.sum()),
+           "ticks_per_env_step": float(ticks.sum()) / max(int(k.sum()), 1)}
     if cap:
         rows = 0
         mism = 0

@@ -42,6 +42,7 @@ def test_state_layout_matches(lib):
     hdr = open(HEADER).read()
     assert f"#define SALP_INFO_DIM {_abi.INFO_DIM}" in hdr
     assert f"#define SALP_MAX_OBSTACLES {_abi.MAX_OBSTACLES}" in hdr
+    assert f"#define SALP_MATH_SELFTEST_ROWS {_abi.MATH_SELFTEST_ROWS}" in hdr
 
 
 def test_default_params_match_python(lib):

@@ -10,7 +10,7 @@ import pytest
 import torch
 
 from golden_util import COMPARED, load_episodes, snapshot_to_state
-from grasp_lab_salp_amd._abi import FIELD, FIELDS, INFO, NUM_FIELDS, default_params
+from grasp_lab_salp_amd._abi import FIELD, FIELDS, INFO, MATH_SELFTEST_ROWS, NUM_FIELDS, default_params
 from grasp_lab_salp_amd.batched_env import BatchedSalpEnv
 from oracle import oracle as orc
 
@@ -67,18 +67,22 @@ def test_device_math_equals_oracle_math():
                         rng.uniform(-1e-4, 1e-4, 2000), rng.uniform(-80, 80, 2000),
                         [0.0, 1.0, -1.0, 0.5, np.pi / 4, np.pi / 2]])
     y = rng.uniform(-3, 3, len(x))
+    # the tick's roll / pitch pair: both short, one short, either NaN / inf
+    xs = np.concatenate([rng.uniform(-0.07, 0.07, 8000), [0.0, -0.0, 0.0625, -0.0625, np.nan, 0.01, np.inf, 0.01]])
+    ys = np.concatenate([rng.uniform(-0.07, 0.07, 8000), [0.0, 0.0, 0.0625, 0.07, 0.01, np.nan, 0.01, -np.inf]])
+    x, y = np.concatenate([x, xs]), np.concatenate([y, ys])
     from grasp_lab_salp_amd import _lib
     import ctypes
     L = _lib.load()
     xd = torch.tensor(x, device="cuda")
     yd = torch.tensor(y, device="cuda")
-    out = torch.empty((12, len(x)), dtype=torch.float64, device="cuda")
+    out = torch.empty((MATH_SELFTEST_ROWS, len(x)), dtype=torch.float64, device="cuda")
     _lib.check(L.salp_math_selftest(ctypes.c_void_p(xd.data_ptr()), ctypes.c_void_p(yd.data_ptr()),
                                     len(x), ctypes.c_void_p(out.data_ptr()), None))
     torch.cuda.synchronize()
     ref = orc.math_selftest(x, y)
     g = _cpu(out)
-    for r in range(12):
+    for r in range(MATH_SELFTEST_ROWS):
         assert np.array_equal(g[r], ref[r], equal_nan=True), f"math row {r}: {np.sum(g[r] != ref[r])} mismatches"
 
 
@@ -99,7 +103,7 @@ def test_shared_reciprocal_division_equals_ieee_division():
     L = _lib.load()
     xd = torch.tensor(x, device="cuda")
     yd = torch.tensor(y, device="cuda")
-    out = torch.empty((12, len(x)), dtype=torch.float64, device="cuda")
+    out = torch.empty((MATH_SELFTEST_ROWS, len(x)), dtype=torch.float64, device="cuda")
     _lib.check(L.salp_math_selftest(ctypes.c_void_p(xd.data_ptr()), ctypes.c_void_p(yd.data_ptr()),
                                     len(x), ctypes.c_void_p(out.data_ptr()), None))
     torch.cuda.synchronize()

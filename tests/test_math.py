@@ -100,3 +100,75 @@ def test_branch_free_sincos_equals_sincos():
     for r_nb, r in ((9, 0), (10, 1)):
         assert np.array_equal(out[r_nb], out[r], equal_nan=True)
         assert np.array_equal(np.signbit(out[r_nb]), np.signbit(out[r]))
+
+
+def _ulps(got, f, xs):
+    exact = np.array([float(f(mpmath.mpf(v))) for v in xs])
+    return ulp_err(got, exact), exact
+
+
+def test_tick_yaw_sincos_within_one_ulp():
+    """sm_sincos_yaw_p (the tick's yaw, product mode): one Cody-Waite stage and
+    the kernels' tail forms; within one ulp over several turns, near every
+    multiple of pi/4 and at the small angles where fdlibm skips the reduction."""
+    rng = np.random.default_rng(3)
+    k = rng.integers(-40, 40, 4000)
+    x = np.concatenate([rng.uniform(-60, 60, 6000), rng.uniform(-0.8, 0.8, 2000), rng.uniform(-1e-3, 1e-3, 500),
+                        k * (math.pi / 4) + rng.uniform(-1e-6, 1e-6, len(k)), [0.0, 1.0, -1.0, math.pi / 2]])
+    out = oracle.math_selftest(x, np.zeros_like(x))
+    # one Cody-Waite stage: within 1e-26 |fn| absolute, so one ulp unless the
+    # result is within 1e-10 |fn| of zero (x = pi/2 itself: cos 6.1e-17)
+    fn = np.maximum(np.abs(np.rint(x * 2 / math.pi)), 1.0)
+    for row, f in ((12, mpmath.sin), (13, mpmath.cos)):
+        e, exact = _ulps(out[row], f, x)
+        assert np.max(np.abs(out[row] - exact) / fn) <= 1e-26 + 0.5 * np.spacing(1.0), row
+        ok = np.abs(exact) > 1e-10 * fn
+        assert np.max(e[ok]) <= 1.0, (row, float(np.max(e[ok])))
+    # fdlibm's sincos agrees bit for bit nearly always
+    assert np.mean(out[12] == out[0]) > 0.9 and np.mean(out[13] == out[1]) > 0.9
+    nan = oracle.math_selftest(np.array([np.nan, np.inf, -np.inf]), np.zeros(3))
+    assert np.isnan(nan[12]).all() and np.isnan(nan[13]).all()
+
+
+def test_tick_roll_pitch_pair():
+    """sm_sincos_rp2: the four-term kernels when neither |angle| exceeds 1/16
+    (or is NaN), within one ulp; fdlibm's sincos for both otherwise."""
+    rng = np.random.default_rng(4)
+    x = np.concatenate([rng.uniform(-0.0625, 0.0625, 4000), rng.uniform(-1e-6, 1e-6, 500), [0.0625, -0.0625, 0.0]])
+    y = rng.uniform(-0.0625, 0.0625, len(x))
+    out = oracle.math_selftest(x, y)
+    for row, f, a in ((14, mpmath.sin, x), (15, mpmath.cos, x), (16, mpmath.sin, y), (17, mpmath.cos, y)):
+        e, exact = _ulps(out[row], f, a)
+        ok = np.abs(exact) > 1e-300
+        assert np.max(e[ok]) <= 1.0, (row, float(np.max(e[ok])))
+    # one angle beyond 1/16: fdlibm for both (rows 0 / 1 are sm_sin / sm_cos of x)
+    xb = np.concatenate([rng.uniform(-0.05, 0.05, 300), rng.uniform(0.07, 2.0, 300)])
+    yb = np.concatenate([rng.uniform(0.07, 2.0, 300), rng.uniform(-0.05, 0.05, 300)])
+    ob = oracle.math_selftest(xb, yb)
+    assert np.array_equal(ob[14], ob[0]) and np.array_equal(ob[15], ob[1])
+    oy = oracle.math_selftest(yb, xb)
+    assert np.array_equal(ob[16], oy[0]) and np.array_equal(ob[17], oy[1])
+    # NaN takes the short kernels (NaN out) and leaves the other angle on them too
+    on = oracle.math_selftest(np.array([np.nan, 0.01]), np.array([0.01, np.nan]))
+    ref = oracle.math_selftest(np.array([0.01]), np.array([0.0]))
+    assert np.isnan(on[14][0]) and np.isnan(on[15][0]) and np.isnan(on[16][1]) and np.isnan(on[17][1])
+    assert on[16][0] == ref[14][0] and on[17][0] == ref[15][0] and on[14][1] == ref[14][0]
+
+
+def test_tick_world_frame_rotation():
+    """sm_world_frame: Rz(psi) Ry(theta) Rx(phi) v applied as three plane
+    rotations equals the matrix product to a few ulp of |v|."""
+    rng = np.random.default_rng(5)
+    x = rng.uniform(-0.06, 0.06, 400)
+    y = rng.uniform(-0.06, 0.06, 400)
+    out = oracle.math_selftest(x, y)
+    for j in range(0, 400, 7):
+        phi, th, psi = (mpmath.mpf(float(x[j])), mpmath.mpf(float(y[j])), mpmath.mpf(float(x[j] + y[j])))
+        Rx = mpmath.matrix([[1, 0, 0], [0, mpmath.cos(phi), -mpmath.sin(phi)], [0, mpmath.sin(phi), mpmath.cos(phi)]])
+        Ry = mpmath.matrix([[mpmath.cos(th), 0, mpmath.sin(th)], [0, 1, 0], [-mpmath.sin(th), 0, mpmath.cos(th)]])
+        Rz = mpmath.matrix([[mpmath.cos(psi), -mpmath.sin(psi), 0], [mpmath.sin(psi), mpmath.cos(psi), 0], [0, 0, 1]])
+        v = mpmath.matrix([float(y[j]), float(x[j]), 1.0])
+        want = Rz * Ry * Rx * v
+        norm = float(mpmath.norm(v))
+        for r in range(3):
+            assert abs(out[18 + r][j] - float(want[r])) <= 4 * np.spacing(norm), (j, r)

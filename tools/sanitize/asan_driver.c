@@ -142,7 +142,7 @@ static void oracle_misc(void) {
     CHECK(oracle_robot_trace(&p, acts, 10, out, 200000) > 0);
     CHECK(oracle_robot_trace(&p, acts, 10, out, 3) < 0);   /* too small: reports, no overflow */
     free(out);
-    double x[5] = {0.0, -0.0, 1e-300, 3.0, -1e5}, y[5] = {1.0, -2.0, 0.0, INFINITY, 7.0}, m[12 * 5];
+    double x[5] = {0.0, -0.0, 1e-300, 3.0, -1e5}, y[5] = {1.0, -2.0, 0.0, INFINITY, 7.0}, m[SALP_MATH_SELFTEST_ROWS * 5];
     oracle_math_selftest(x, y, 5, m);
 }
 
