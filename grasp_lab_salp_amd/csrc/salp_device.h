@@ -334,16 +334,20 @@ SD Geo make_geo_shape(const Params& P, const Core& c, double L, double W, double
 SD void jet_rates(const Params& P, double V, double pV, double wm, bool g32, bool pv32, Geo& g) {
     const bool b32 = g32 && pv32;
     double pwm = r32(sel(pv32, P.density) * pV, pv32);
-    /* Both dtypes without a branch.  A float32 quotient is the float64
-     * quotient of the float32 operands rounded to float32 (double rounding is
-     * exact here: 53 >= 2*24 + 2), so it shares the float64 reciprocals. */
-    const Rcp rdt32 = rcp_of(sel(true, DT)), ra32 = rcp_of(sel(true, P.nozzle_area));
-    const double mr32 = r32(qdiv(r32(wm - pwm, true), rdt32), true);
-    const double sp32 = r32(qdiv(r32(qdiv(r32(V - pV, true), rdt32), true), ra32), true);
-    const double mr64 = div_dt(wm - pwm);
-    const double sp64 = qdiv(div_dt(V - pV), rcp_of(P.nozzle_area));
-    g.mr = b32 ? mr32 : mr64;
-    g.speed = b32 ? sp32 : sp64;
+    g.mr = div_dt(wm - pwm);
+    g.speed = qdiv(div_dt(V - pV), rcp_of(P.nozzle_area));
+    /* The float32 arm only where a lane of the wave holds the float32 body on
+     * two ticks in a row (REFILL past refill_time, ~2.5 % of the ticks).  A
+     * float32 quotient is the float64 quotient of the float32 operands rounded
+     * to float32 (double rounding is exact here: 53 >= 2*24 + 2), so it
+     * shares the float64 reciprocals. */
+    if (__any(b32)) {
+        const Rcp rdt32 = rcp_of(sel(true, DT)), ra32 = rcp_of(sel(true, P.nozzle_area));
+        const double mr32 = r32(qdiv(r32(wm - pwm, true), rdt32), true);
+        const double sp32 = r32(qdiv(r32(qdiv(r32(V - pV, true), rdt32), true), ra32), true);
+        g.mr = b32 ? mr32 : g.mr;
+        g.speed = b32 ? sp32 : g.speed;
+    }
 }
 /* The correctly rounded reciprocals 1/m, 1/I0, 1/I1 of the dynamics' two
  * solves (F/m, tau/I; product mode: F * (1/m), the oracle's robot_newton /
@@ -710,11 +714,11 @@ SD bool tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     double mv0 = m * h.v0, mv1 = m * h.v1, mv2 = m * h.v2;
     double cf0 = -cross_c(h.w1, mv2, h.w2, mv1), cf1 = -cross_c(h.w2, mv0, h.w0, mv2),
            cf2 = -cross_c(h.w0, mv1, h.w1, mv0);
-    /* drag force (src/dynamics.py:110-116) */
-    double vn = np_norm3(h.v0, h.v1, h.v2);
-    double df0 = sm_mad(g.kc0 * h.v0, dfr, g.kc0 * vn * h.v0);
-    double df1 = sm_mad(g.kc1 * h.v1, dfr, g.kc1 * vn * h.v1);
-    double df2 = sm_mad(g.kc1 * h.v2, dfr, g.kc1 * vn * h.v2);
+    /* drag force (src/dynamics.py:110-116); product mode: (k C v) (|v| + ratio) */
+    const double vnr = np_norm3(h.v0, h.v1, h.v2) + dfr;
+    double df0 = (g.kc0 * h.v0) * vnr;
+    double df1 = (g.kc1 * h.v1) * vnr;
+    double df2 = (g.kc1 * h.v2) * vnr;
     /* jet force, JET phase only (src/robot.py:937-951, src/dynamics.py:87-101) */
     const bool jet = !SETTLED && h.phase == JET;
     double jf0 = jet ? g.mr * (h.d0 * g.speed) * -cd : 0.0;
@@ -753,11 +757,12 @@ SD bool tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     double iw0 = I0 * h.w0, iw1 = I1 * h.w1, iw2 = I1 * h.w2;
     double ct0 = -cross_c(h.w1, iw2, h.w2, iw1), ct1 = -cross_c(h.w2, iw0, h.w0, iw2),
            ct2 = -cross_c(h.w0, iw1, h.w1, iw0);
-    /* drag torque (src/dynamics.py:119-128) */
-    double wn = np_norm3(h.w0, h.w1, h.w2);
-    double dt0 = sm_mad(g.ra0 * h.w0 * h.W, dtr, g.ra0 * wn * h.w0 * g.dimx);
-    double dt1 = sm_mad(g.ra1 * h.w1 * h.W, dtr, g.ra1 * wn * h.w1 * g.dimy);
-    double dt2 = sm_mad(g.ra1 * h.w2 * h.W, dtr, g.ra1 * wn * h.w2 * g.dimy);
+    /* drag torque (src/dynamics.py:119-128); product mode: (C k A w) (|w| dims + width ratio) */
+    const double wn = np_norm3(h.w0, h.w1, h.w2), wr = h.W * dtr;
+    const double sx = sm_fma(wn, g.dimx, wr), sy = sm_fma(wn, g.dimy, wr);
+    double dt0 = (g.ra0 * h.w0) * sx;
+    double dt1 = (g.ra1 * h.w1) * sy;
+    double dt2 = (g.ra1 * h.w2) * sy;
     /* jet torque r x F, r = (mid_x - L/2, 0, 0) (src/robot.py:931-935) */
     double jt1 = -(g.rx * jf2), jt2 = g.rx * jf1;
     /* deformation torque -(dI/dt) w; prev_I <- I (src/robot.py:888-896) */

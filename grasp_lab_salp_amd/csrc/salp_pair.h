@@ -188,10 +188,10 @@ SD bool step_a_newton(HotA& h, const Params& P, const PreA& g) {
     double mv0 = m * h.v0, mv1 = m * h.v1, mv2 = m * h.v2;
     double cf0 = -cross_c(h.w1, mv2, h.w2, mv1), cf1 = -cross_c(h.w2, mv0, h.w0, mv2),
            cf2 = -cross_c(h.w0, mv1, h.w1, mv0);
-    double vn = np_norm3(h.v0, h.v1, h.v2);
-    double df0 = sm_mad(h.kc0 * h.v0, DRAG_FORCE_RATIO, h.kc0 * vn * h.v0);
-    double df1 = sm_mad(h.kc1 * h.v1, DRAG_FORCE_RATIO, h.kc1 * vn * h.v1);
-    double df2 = sm_mad(h.kc1 * h.v2, DRAG_FORCE_RATIO, h.kc1 * vn * h.v2);
+    const double vnr = np_norm3(h.v0, h.v1, h.v2) + DRAG_FORCE_RATIO;
+    double df0 = (h.kc0 * h.v0) * vnr;
+    double df1 = (h.kc1 * h.v1) * vnr;
+    double df2 = (h.kc1 * h.v2) * vnr;
     const double mrt = SETTLED ? 0.0 : h.mr;
     double am0 = m * AMF0, am1 = m * AMF1, am2 = m * AMF2;
     double amr0 = mrt * AMRF, amr1 = mrt * AMRF, amr2 = mrt * AMRF;
@@ -282,10 +282,11 @@ SD void step_b1(HotB& h, const Params& P) {
     double iw0 = I0 * h.w0, iw1 = I1 * h.w1, iw2 = I1 * h.w2;
     double ct0 = -cross_c(h.w1, iw2, h.w2, iw1), ct1 = -cross_c(h.w2, iw0, h.w0, iw2),
            ct2 = -cross_c(h.w0, iw1, h.w1, iw0);
-    double wn = np_norm3(h.w0, h.w1, h.w2);
-    double dt0 = sm_mad(h.ra0 * h.w0 * h.W, DRAG_TORQUE_RATIO, h.ra0 * wn * h.w0 * h.dimx);
-    double dt1 = sm_mad(h.ra1 * h.w1 * h.W, DRAG_TORQUE_RATIO, h.ra1 * wn * h.w1 * h.dimy);
-    double dt2 = sm_mad(h.ra1 * h.w2 * h.W, DRAG_TORQUE_RATIO, h.ra1 * wn * h.w2 * h.dimy);
+    const double wn = np_norm3(h.w0, h.w1, h.w2), wr = h.W * DRAG_TORQUE_RATIO;
+    const double sx = sm_fma(wn, h.dimx, wr), sy = sm_fma(wn, h.dimy, wr);
+    double dt0 = (h.ra0 * h.w0) * sx;
+    double dt1 = (h.ra1 * h.w1) * sy;
+    double dt2 = (h.ra1 * h.w2) * sy;
     double ir0 = 0.0, ir1 = 0.0, ir2 = 0.0;
     if (!SETTLED) {
         ir0 = div_dt(I0 - h.pI0);

@@ -512,9 +512,15 @@ static V3 compute_drag_force(double density, V3 area, V3 cd, V3 vel, double rati
     V3 ka = vmuls(area, k);
     if (area32) /* python float * float32 array -> float32 */
         for (int i = 0; i < 3; ++i) ka.v[i] = (double)((float)k * (float)area.v[i]);
+#if SALP_FMA
+    /* product mode (round 5): (ka cd v) (|v| + ratio), the device's form */
+    V3 kv = vmul(vmul(ka, cd), vel);
+    return vmuls(kv, vn + ratio);
+#else
     V3 fq = vmul(vmuls(vmul(ka, cd), vn), vel);
     V3 fl = vmul(vmul(ka, cd), vel);
     return vmad(fl, ratio, fq);   /* fq + fl * ratio */
+#endif
 }
 /* src/dynamics.py:119-128 */
 static V3 compute_drag_torque(double density, V3 rcd, V3 area, V3 w, double width, double length,
@@ -523,9 +529,17 @@ static V3 compute_drag_torque(double density, V3 rcd, V3 area, V3 w, double widt
     V3 dims = f32 ? v3((double)cubef((float)width), (double)cubef((float)length), (double)cubef((float)length))
                   : v3(sm_cube(width), sm_cube(length), sm_cube(length));
     double k = -0.5 * density;
+#if SALP_FMA
+    /* product mode (round 5): (rcd k A w) (|w| dims + width ratio), the device's form */
+    V3 aw = vmul(vmul(vmuls(rcd, k), area), w);
+    const double wr = width * ratio;
+    return v3(aw.v[0] * sm_fma(wn, dims.v[0], wr), aw.v[1] * sm_fma(wn, dims.v[1], wr),
+              aw.v[2] * sm_fma(wn, dims.v[2], wr));
+#else
     V3 tq = vmul(vmul(vmuls(vmul(vmuls(rcd, k), area), wn), w), dims);
     V3 tl = vmuls(vmul(vmul(vmuls(rcd, k), area), w), width);
     return vmad(tl, ratio, tq);   /* tq + tl * ratio */
+#endif
 }
 /* src/dynamics.py:131-141 */
 static V3 compute_added_mass_force(M3 mass, M3 amc, M3 mass_rate, M3 amrc, V3 acc, V3 w, V3 vel) {
