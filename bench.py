@@ -111,7 +111,8 @@ def parse(argv=None):
     ap.add_argument("--n-envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--tick-budget", type=int, default=8192, help="physics ticks per env per launch")
     ap.add_argument("--capacity", type=int, default=16, help="rollout-buffer slots per env")
-    ap.add_argument("--chunk", type=int, default=128, help="ticks between env-step boundaries")
+    ap.add_argument("--chunk", type=int, default=64,
+                    help="ticks between env-step boundaries (64 with q = 560: profiles/r5_experiments.md r5j-r5k)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")

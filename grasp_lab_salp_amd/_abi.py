@@ -6,9 +6,9 @@ drift apart silently.
 """
 import ctypes
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 # rows of salp_math_selftest's output (include/salp.h)
-MATH_SELFTEST_ROWS = 21
+MATH_SELFTEST_ROWS = 23
 MAX_OBSTACLES = 4
 OBS_DIM_MAX = 6 + 2 * MAX_OBSTACLES
 

@@ -129,6 +129,7 @@ SIGNATURES = {
     "salp_lstm_step_backward": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32] + [_V] * 11),
     "salp_set_lockstep_order": (ctypes.c_int, [_H, ctypes.c_int]),
     "salp_set_rollout_kernel": (ctypes.c_int, [_H, ctypes.c_int]),
+    "salp_pair_timeouts": (ctypes.c_int, [_H, ctypes.POINTER(ctypes.c_uint64), _V]),
     "salp_robot_reset": (ctypes.c_int, [_H, _V, _V]),
     "salp_nozzle_set_angles": (ctypes.c_int, [_H, _V, _V]),
     "salp_nozzle_solve": (ctypes.c_int, [_H, _V, ctypes.c_int, _V]),
@@ -165,11 +166,17 @@ def load(path=LIB_PATH):
         raise SalpError(f"{path} not found: build it with `python -m grasp_lab_salp_amd.build` "
                         "(there is no CPU fallback for the simulator)")
     L = ctypes.CDLL(path)
+    # SALP_AB_OLD_ABI=1: an A/B run against a library of an earlier round (its
+    # missing newer entry points stay unbound, its older ABI number passes);
+    # the state and trace layouts must still match
+    old_ok = os.environ.get("SALP_AB_OLD_ABI") == "1"
     for name, (res, args) in SIGNATURES.items():
+        if old_ok and not hasattr(L, name):
+            continue
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.salp_abi_version() != ABI_VERSION:
+    if L.salp_abi_version() != ABI_VERSION and not old_ok:
         raise SalpError("libsalp ABI version mismatch")
     if L.salp_num_fields() != NUM_FIELDS:
         raise SalpError("libsalp state layout does not match grasp_lab_salp_amd._abi")

@@ -193,7 +193,22 @@ class BatchedSalpEnv:
         identical in every mode."""
         self._check(_lib.load().salp_set_rollout_kernel(self._h, int(mode)))
 
-    def rollout(self, tick_budget, buffers=None, steps_done=None, max_steps=0, chunk=128):
+    def pair_timeouts(self):
+        """Partner waits of the two-wave kernel that gave up since the last
+        call (salp_pair_timeouts; synchronises the stream).  Nonzero means some
+        env's results of those launches are invalid."""
+        c = ctypes.c_uint64(0)
+        self._check(_lib.load().salp_pair_timeouts(self._h, ctypes.byref(c), self._stream()))
+        return int(c.value)
+
+    def check_pair(self):
+        """Raise SalpError if a two-wave launch since the last check gave up
+        on a partner wave (its envs' results are invalid)."""
+        n = self.pair_timeouts()
+        if n:
+            raise _lib.SalpError(f"k_rollout_pair: {n} partner wait(s) timed out; the affected envs' results are invalid")
+
+    def rollout(self, tick_budget, buffers=None, steps_done=None, max_steps=0, chunk=64):
         """Chained random-action rollout: each env runs ``tick_budget`` physics
         ticks, completing as many env-steps as fit (auto-reset).  ``buffers`` is
         an optional dict of preallocated device tensors {obs [cap,n,obs_dim]

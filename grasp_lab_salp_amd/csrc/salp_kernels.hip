@@ -684,6 +684,39 @@ __device__ __noinline__ bool lane_boundary_call(const RolloutArgs* a, double* sp
     return lane_boundary<RAND, POL>(*a, salp::SpillSlot{spp}, i, *pending, *active, *steps, c32p);
 }
 
+// SALP_ROLLOUT_PROF=1 (experiment builds only, tools/rollout_phase_prof.py):
+// per wave, s_memtime cycles and loop iterations of each part of k_rollout's
+// chunk loop, summed over the launch's waves into g_roll_prof (read back by
+// salp_debug_rollout_prof): boundary + re-seat, full ticks, steady ticks,
+// settled ticks.
+#ifndef SALP_ROLLOUT_PROF
+#define SALP_ROLLOUT_PROF 0
+#endif
+enum { RP_BOUNDARY, RP_FULL, RP_STEADY, RP_SETTLED, RP_BARRIER, RP_RESEAT, RP_N };
+__device__ unsigned long long g_roll_prof[2][RP_N];   // [cycles | iterations][part]
+struct RollProf {
+    unsigned long long cyc[RP_N] = {}, its[RP_N] = {};
+    unsigned long long t = 0;
+    __device__ __forceinline__ void start() {
+        if (SALP_ROLLOUT_PROF) t = __builtin_amdgcn_s_memtime();
+    }
+    __device__ __forceinline__ void lap(int part, int64_t iterations = 0) {
+        if (SALP_ROLLOUT_PROF) {
+            const unsigned long long now = __builtin_amdgcn_s_memtime();
+            cyc[part] += now - t;
+            its[part] += (unsigned long long)iterations;
+            t = now;
+        }
+    }
+    __device__ __forceinline__ void flush() {
+        if (SALP_ROLLOUT_PROF && (threadIdx.x & 63) == 0)
+            for (int k = 0; k < RP_N; ++k) {
+                atomicAdd(&g_roll_prof[0][k], cyc[k]);
+                atomicAdd(&g_roll_prof[1][k], its[k]);
+            }
+    }
+};
+
 #if SALP_ROLLOUT_RESEAT
 template <bool RAND, bool POL>
 __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
@@ -714,6 +747,8 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
     // slots past the end of the batch hold no env: never active, never stored
     if (!active) h.b2 = -INFINITY;
     bool all_done = false;   // no env of the workgroup has an env-step left (max_steps)
+    RollProf prof;
+    prof.start();
     for (int64_t c = 0;; ++c) {
         const bool last = c == A.n_chunks || all_done;
         const salp::SpillSlot sp{s_spill + s};
@@ -748,7 +783,9 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
             s_mask[b][lane >> 6] = ballot;
             s_amask[b][lane >> 6] = aballot;
         }
+        prof.lap(RP_BOUNDARY);
         __syncthreads();
+        prof.lap(RP_BARRIER);
         uint64_t m[kBlock / 64];
         int n_uns = 0;
         uint64_t any_active = 0;
@@ -779,6 +816,7 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
         }
         if (!active) h.b2 = -INFINITY;   // a finished lane (or an empty slot) ticks no more
         if (all_done) continue;          // next pass stores the state and leaves
+        prof.lap(RP_RESEAT);
         const salp::Cache32 c32{s_cache32 + s};
         const Params PV = salp::pin_params(P);
         int32_t k = 0;
@@ -786,6 +824,7 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
             if (__all(!(h.ct < h.b2) || salp::next_tick_steady(h, PV))) break;
             if (h.ct < h.b2) salp::tick<false, RAND, true>(h, PV, c32);
         }
+        prof.lap(RP_FULL, k);
         const int32_t ks = (int32_t)(((int64_t)(A.chunk - k) * A.steady_q8) >> 8);
         // steady ticks until every ticking lane of the wave is settled, then
         // settled ticks (salp_device.h tick; lanes whose cycle has ended idle)
@@ -798,9 +837,13 @@ __global__ __launch_bounds__(kBlock) void k_rollout(RolloutArgs A) {
                 break;
             }
         }
+        prof.lap(RP_STEADY, j);
+        const int32_t j0 = j;
         for (; j < ks; ++j)
             if (h.ct < h.b2) salp::tick<false, RAND, true, true, true>(h, PV, c32);
+        prof.lap(RP_SETTLED, j - j0);
     }
+    prof.flush();
     if (A.B.steps_done && i < P.n) A.B.steps_done[i] = steps;
 }
 #else
@@ -877,8 +920,11 @@ constexpr int kXchBase = 4 * kXchAB * 64;                           // first dou
 constexpr int kXchDoubles = kXchBase + 4 * kXchBA * 64;
 static_assert(kXchDoubles <= salp::SPILL_N * kPairEnvs, "the packets live in the spill slots' LDS");
 // A wave gives up on its partner after this many polls (s_sleep 1 = 64 cycles
-// each, ~0.1 s): the kernel always ends (a broken pair gives garbage, which the
-// parity tests see, instead of a hung GPU); counted in g_pair_timeouts.
+// each: 2^21 x 64 = 134 M cycles, ~56 ms at 2.4 GHz, against ~1 us for a
+// tick's round trip and ~50 us for the longest legitimate wait, a boundary
+// round of value jobs): the kernel always ends instead of hanging the GPU.
+// Such an env's results are invalid; g_pair_timeouts counts the give-ups and
+// salp_pair_timeouts reads it (the Python layer raises on a nonzero count).
 constexpr int kPairSpin = 1 << 21;
 __device__ unsigned int g_pair_timeouts;
 
@@ -1467,6 +1513,8 @@ __global__ void k_math_selftest(const double* x, const double* y, int64_t n, dou
     out[18 * n + i] = wf[0];
     out[19 * n + i] = wf[1];
     out[20 * n + i] = wf[2];
+    out[21 * n + i] = sm_atan(x[i]);
+    out[22 * n + i] = sm_atan_ref(x[i]);
 }
 
 const char* const kFieldNames[SALP_NUM_FIELDS] = {
@@ -1531,13 +1579,15 @@ unsigned blocks_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 // k_rollout's steady ticks per full tick of a wave's chunk budget (x256): a
 // steady tick costs ~0.8 of a full one in the round-2 kernel (q = 360,
 // profiles/r2_experiments.md r2l-r2o); with the fused arithmetic and settled
-// ticks ~0.65 (q = 480 best of 360..580, profiles/r3_experiments.md r3f).
-// SALP_STEADY_Q8 overrides it for tuning runs; it changes throughput only.
+// ticks ~0.65 (q = 480 best of 360..580, profiles/r3_experiments.md r3f);
+// round 5's cheaper settled tick (1 500 vs 3 760 cycles a full one, phase
+// profile r5f) moved it to q = 560 (480..900 swept, profiles/r5_experiments.md
+// r5g).  SALP_STEADY_Q8 overrides it for tuning runs; it changes throughput only.
 int32_t rollout_steady_q8() {
     static const int32_t q = [] {
         const char* e = std::getenv("SALP_STEADY_Q8");
         const long v = e ? std::strtol(e, nullptr, 10) : 0;
-        return (int32_t)(v > 0 && v < (1 << 16) ? v : 480);
+        return (int32_t)(v > 0 && v < (1 << 16) ? v : 560);
     }();
     return q;
 }
@@ -1839,7 +1889,7 @@ int salp_step_random(SalpEnv* h, int32_t n_steps, double* reward_sum_out, void* 
         static const int32_t chunk = [] {   // SALP_STEP_RANDOM_CHUNK: tuning runs only
             const char* e = std::getenv("SALP_STEP_RANDOM_CHUNK");
             const long v = e ? std::strtol(e, nullptr, 10) : 0;
-            return (int32_t)(v > 0 && v < 4096 ? v : 128);
+            return (int32_t)(v > 0 && v < 4096 ? v : 64);
         }();
         // bound: n_steps cycles of the longest legitimate length (the lock-step guard)
         const int64_t n_chunks = ((int64_t)n_steps * kMaxTicksPerCycle + chunk - 1) / chunk;
@@ -1859,7 +1909,9 @@ int salp_rollout(SalpEnv* h, int64_t tick_budget, const SalpRolloutBuffers* buf,
     SalpRolloutBuffers b{};
     if (buf) b = *buf;
     if (b.capacity < 0) return fail(h, SALP_EINVAL, "salp_rollout: capacity < 0");
-    int32_t chunk = b.chunk > 0 ? b.chunk : 128;
+    // chunk 64 with q = 560 (round 5: the cheaper settled tick made shorter
+    // chunks pay; 48 / 64 / 80 / 96 / 112 / 128 swept, profiles/r5_experiments.md r5j-r5k)
+    int32_t chunk = b.chunk > 0 ? b.chunk : 64;
     int64_t n_chunks = (tick_budget + chunk - 1) / chunk;
     RolloutArgs args{h->state, h->dp, n_chunks, chunk, rollout_steady_q8(), b.max_steps, b, nullptr, 0, 0};
     return launch_chained(h, args, false, (hipStream_t)stream, "k_rollout");
@@ -1879,7 +1931,7 @@ int salp_collect(SalpEnv* h, const SalpPolicyRollout* r, void* stream) {
     SalpRolloutBuffers b{};
     b.steps_done = h->step_counts;
     b.max_steps = r->n_steps;
-    // Longer chunks than the rollout's 128: every wave evaluates the policy at
+    // Longer chunks than the rollout's 64: every wave evaluates the policy at
     // most once per chunk, and that evaluation is on its critical path
     // (k_rollout, 65 536 envs, M env-steps/s by chunk 128 / 192 / 256 / 384 /
     // 512 / 768: 26.3 / 28.3 / 28.3 / 29.2 / 28.6 / 24.6; profiles/
@@ -1947,6 +1999,15 @@ int salp_set_lockstep_order(SalpEnv* h, int mode) {
     return SALP_OK;
 }
 
+#if SALP_ROLLOUT_PROF
+// experiment builds only (not in include/salp.h): read and clear g_roll_prof
+int salp_debug_rollout_prof(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_roll_prof), sizeof(g_roll_prof)) != hipSuccess) return -1;
+    static const unsigned long long zero[2][RP_N] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_roll_prof), zero, sizeof zero) == hipSuccess ? 0 : -1;
+}
+#endif
+
 #if SALP_PAIR_PROF
 // experiment builds only (not in include/salp.h): read and clear g_pair_prof
 int salp_debug_pair_prof(unsigned long long* out) {
@@ -1955,6 +2016,20 @@ int salp_debug_pair_prof(unsigned long long* out) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_pair_prof), zero, sizeof zero) == hipSuccess ? 0 : -1;
 }
 #endif
+
+int salp_pair_timeouts(SalpEnv* h, uint64_t* count_out, void* stream) {
+    if (!h || !count_out) return fail(h, SALP_EINVAL, "salp_pair_timeouts: null argument");
+    unsigned int c = 0;
+    const hipStream_t s = (hipStream_t)stream;
+    hipError_t e = hipMemcpyFromSymbolAsync(&c, HIP_SYMBOL(g_pair_timeouts), sizeof c, 0, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    static const unsigned int zero = 0;
+    if (e == hipSuccess && c != 0) e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_pair_timeouts), &zero, sizeof zero, 0,
+                                                               hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    *count_out = c;
+    return check_hip(h, e, "salp_pair_timeouts");
+}
 
 int salp_set_rollout_kernel(SalpEnv* h, int mode) {
     if (!h) return fail(nullptr, SALP_EINVAL, "salp_set_rollout_kernel: null handle");

@@ -373,7 +373,44 @@ SM_QUAL double sm_cos(double x) { double s, c; sm_sincos(x, &s, &c); return c; }
 SM_QUAL double sm_tan(double x) { double s, c; sm_sincos(x, &s, &c); return s / c; }
 
 /* ----------------------------------------------------- atan family */
+/* fdlibm's atan: the branchy original (sm_atan_ref, kept as the test's
+ * reference) and the form the product uses, with its five argument ranges
+ * chosen by selects and ONE division instead of a branch per range (a wave
+ * whose lanes span the ranges ran every range's path: env-step boundaries
+ * take five atan2 per env, src/robot.py:79-93, src/salp_robot_env.py:370,
+ * 668).  Every operation is the original's on the same operands (x / 1 is
+ * exact), so the two are equal bit for bit (tests/test_math.py). */
 SM_QUAL double sm_atan(double x) {
+    const double atanhi0 = 4.63647609000806093515e-01, atanhi1 = 7.85398163397448278999e-01,
+                 atanhi2 = 9.82793723247329054082e-01, atanhi3 = 1.57079632679489655800e+00;
+    const double atanlo0 = 2.26987774529616870924e-17, atanlo1 = 3.06161699786838301793e-17,
+                 atanlo2 = 1.39033110312309984516e-17, atanlo3 = 6.12323399573676603587e-17;
+    const double aT0 = 3.33333333333329318027e-01, aT1 = -1.99999999998764832476e-01,
+                 aT2 = 1.42857142725034663711e-01, aT3 = -1.11111104054623557880e-01,
+                 aT4 = 9.09088713343650656196e-02, aT5 = -7.69187620504482999495e-02,
+                 aT6 = 6.66107313738753120669e-02, aT7 = -5.83357013379057348645e-02,
+                 aT8 = 4.97687799461593236017e-02, aT9 = -3.65315727442169155270e-02,
+                 aT10 = 1.62858201153657823623e-02;
+    const int32_t hx = sm_hi(x), ix = hx & 0x7fffffff;
+    const double ax = fabs(x);
+    const int small = ix < 0x3fdc0000;                  /* |x| < 0.4375: id -1, no reduction */
+    const int r0 = ix < 0x3fe60000, r1 = ix < 0x3ff30000, r2 = ix < 0x40038000;
+    /* id 0: (2x - 1) / (2 + x); 1: (x - 1) / (x + 1); 2: (x - 1.5) / (1 + 1.5x); 3: -1 / x */
+    const double num = small ? x : r0 ? 2.0 * ax - 1.0 : r1 ? ax - 1.0 : r2 ? ax - 1.5 : -1.0;
+    const double den = small ? 1.0 : r0 ? 2.0 + ax : r1 ? ax + 1.0 : r2 ? 1.0 + 1.5 * ax : ax;
+    const double t = num / den;
+    const double z = t * t, w = z * z;
+    const double s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+    const double s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+    const double hi = r0 ? atanhi0 : r1 ? atanhi1 : r2 ? atanhi2 : atanhi3;
+    const double lo = r0 ? atanlo0 : r1 ? atanlo1 : r2 ? atanlo2 : atanlo3;
+    const double zr = hi - ((t * (s1 + s2) - lo) - t);
+    const double big = atanhi3 + atanlo3;               /* |x| >= 2^66 */
+    double r = small ? (ix < 0x3e400000 ? x : t - t * (s1 + s2)) : (hx < 0 ? -zr : zr);
+    if (ix >= 0x44100000) r = hx < 0 ? -big : big;
+    return r;
+}
+SM_QUAL double sm_atan_ref(double x) {
     const double atanhi[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01,
                               9.82793723247329054082e-01, 1.57079632679489655800e+00};
     const double atanlo[4] = {2.26987774529616870924e-17, 3.06161699786838301793e-17,

@@ -400,6 +400,7 @@ class PPO:
         self._graph = None
         self._graph_warm = 0
         self._epoch_graph = None   # fused step, one GPU: one graph per chunk of minibatches
+        self._rem_graph = None     # and one for the epoch's last m % chunk minibatches
         self.max_graph_minibatches = max(1, int(max_graph_minibatches))
         self._g_clip = None
         self._collect_stream = None
@@ -758,27 +759,29 @@ class PPO:
         return dict(zip(("pg_loss", "vf_loss", "entropy", "clip_frac"), vals))
 
     def _graph_chunk(self, m):
-        """Minibatches per captured graph: the largest divisor of the epoch's
-        `m` minibatches that is at most max_graph_minibatches (a graph's node
-        count and its capture loop stay bounded whatever n_steps x n_envs /
-        batch_size is: SB3's default batch_size 64 at 32 768 envs x 2 048 steps
-        would otherwise be a million minibatches in one graph)."""
-        cap = min(m, self.max_graph_minibatches)
-        return max(d for d in range(1, cap + 1) if m % d == 0)
+        """Minibatches per captured graph: the epoch's `m` minibatches, at most
+        max_graph_minibatches (a graph's node count and its capture loop stay
+        bounded whatever n_steps x n_envs / batch_size is: SB3's default
+        batch_size 64 at 32 768 envs x 2 048 steps would otherwise be a million
+        minibatches in one graph).  m % chunk minibatches are left for a second,
+        shorter graph (_train_epoch_graphs)."""
+        return min(m, self.max_graph_minibatches)
 
     def _train_epoch_graphs(self):
         """train() for the fused step on one GPU: every minibatch reads its rows
         from a slice of one persistent index buffer, so a chunk of C
         minibatches (4 kernels each) is one HIP graph, captured once and
-        replayed M / C times per epoch (M minibatches per epoch; C = M, one
+        replayed M // C times per epoch (M minibatches per epoch; C = M, one
         graph per epoch, unless M exceeds max_graph_minibatches), each time
         after the next C x batch_size indices of the epoch's permutation are
-        copied into it.  The same kernels in the same order as minibatch by
-        minibatch (no per-minibatch launch from Python)."""
+        copied into it; the last M % C minibatches are a second graph, captured
+        once too.  The same kernels in the same order as minibatch by minibatch
+        (no per-minibatch launch from Python)."""
         N = self.n_steps * self.n_envs
         bs = self.batch_size
         m = N // bs
         c = self._graph_chunk(m)
+        rem = m % c
         fresh = False
         if self._epoch_graph is None or self._g_clip != self._clip():
             if self._epoch_graph is None:
@@ -796,6 +799,13 @@ class PPO:
                 for s in range(0, c * bs, bs):
                     self._fused_minibatch(self._gperm[s:s + bs], self._g_acc)
             self._epoch_graph = g
+            self._rem_graph = None
+            if rem:   # the ragged tail: a graph of its own over the head of the same buffer
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr, capture_error_mode=_CAPTURE_MODE):
+                    for s in range(0, rem * bs, bs):
+                        self._fused_minibatch(self._gperm[s:s + bs], self._g_acc)
+                self._rem_graph = gr
             fresh = True
         for e in range(self.n_epochs):
             if not (fresh and e == 0):   # the capture's permutation serves the first epoch
@@ -804,6 +814,9 @@ class PPO:
                 if c != m and not (fresh and e == 0 and k == 0):
                     self._gperm.copy_(self._perm[k * c * bs:(k + 1) * c * bs])
                 self._epoch_graph.replay()
+            if rem:
+                self._gperm[:rem * bs].copy_(self._perm[(m - rem) * bs:m * bs])
+                self._rem_graph.replay()
         vals = (self._g_acc / (self.n_epochs * m)).tolist()
         self._g_acc.zero_()
         return dict(zip(("pg_loss", "vf_loss", "entropy", "clip_frac"), vals))
@@ -853,6 +866,11 @@ class PPO:
             self.timing["train_s"] += ev[2].elapsed_time(end) / 1e3
             self.num_timesteps += self.n_steps * self.n_envs
             it += 1
+            if self.collect == "chained":
+                # the two-wave collection kernel never hangs the GPU: a wave that
+                # waits for its partner in vain gives up, and its envs' buffers
+                # are invalid (include/salp.h salp_pair_timeouts)
+                self.sim.check_pair()
             ret_sum, n_ep, n_succ, len_sum = self._ep_stats.tolist()
             row = {"iteration": len(self.history) + 1, "timesteps": self.num_timesteps, **self.logger,
                    "episodes": int(n_ep), "ep_return_mean": ret_sum / n_ep if n_ep else None,

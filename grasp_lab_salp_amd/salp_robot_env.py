@@ -72,6 +72,15 @@ def draw_target(width, height, strategy="random", current_pos=None, center=None,
     return target.astype(np.float32)
 
 
+def _frozen(a):
+    """A read-only copy of an array-like attribute (None stays None)."""
+    if a is None:
+        return None
+    a = np.array(a, copy=True)
+    a.flags.writeable = False
+    return a
+
+
 def draw_obstacles(width, height, num_obstacles, obstacle_radius, target):
     """_generate_obstacles (src/salp_robot_env.py:535-559): rejection sampling
     from the global np.random, at most 200 tries per obstacle; the list can
@@ -160,10 +169,14 @@ class SalpRobotEnv(GymEnv):
     # steps - placing a target or obstacles by hand, as the edge-case episodes
     # of tests/golden/make_golden.py do - changes what the next step computes,
     # so here the setters write the value through to the env's device state.
-    # The observation is recomputed by the next step() / reset().
+    # The observation is recomputed by the next step() / reset().  Only a whole
+    # assignment reaches the device: the getters hand out read-only copies (a
+    # tuple of read-only arrays for the obstacles), so an in-place edit
+    # (env.obstacles[0][0] = ..., env.obstacles.append(...)) raises instead of
+    # silently changing a host copy the simulation never reads.
     @property
     def target_point(self):
-        return self._target_point
+        return _frozen(self._target_point)
 
     @target_point.setter
     def target_point(self, value):
@@ -173,7 +186,7 @@ class SalpRobotEnv(GymEnv):
 
     @property
     def obstacles(self):
-        return self._obstacles
+        return tuple(_frozen(o) for o in self._obstacles)
 
     @obstacles.setter
     def obstacles(self, value):

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define SALP_ABI_VERSION 9
+#define SALP_ABI_VERSION 10
 
 #define SALP_MAX_OBSTACLES 4
 #define SALP_OBS_DIM_MAX (6 + 2 * SALP_MAX_OBSTACLES)
@@ -101,7 +101,7 @@ typedef struct SalpRolloutBuffers {
     int64_t* steps_done;   /* [n_envs] completed env-steps counter (in/out)    */
     int64_t max_steps;     /* >0: a lane starts no env-step once steps_done
                             * reaches it (fixed-length rollouts, n_steps)     */
-    int32_t chunk;         /* ticks between env-step boundaries (0 = 128)     */
+    int32_t chunk;         /* ticks between env-step boundaries (0 = 64)      */
     int32_t reserved;
     float* obs_before;     /* [capacity][n_envs][obs_dim]  the observation the
                             * step's action was taken from (SB3 RolloutBuffer
@@ -234,6 +234,14 @@ int salp_set_lockstep_order(SalpEnv* h, int mode);
  * with a randomisation switch on the chained calls use k_rollout.  Results per
  * env are identical in every mode. */
 int salp_set_rollout_kernel(SalpEnv* h, int mode);
+/* Partner waits of k_rollout_pair that gave up (ABI 10): the two waves of an
+ * env meet once per tick; a wave that polls for its partner ~56 ms in vain
+ * stops waiting, so that the kernel always ends, and that env's results of the
+ * launch are then invalid.  Reads (synchronising `stream`) and clears the
+ * count of such waits since the previous call, over every launch of the
+ * process; 0 is the only good answer (the Python layer raises otherwise).
+ * Diagnostic with no reference counterpart. */
+int salp_pair_timeouts(SalpEnv* h, uint64_t* count_out, void* stream);
 
 /* GAE / returns over a rollout buffer: stable_baselines3's
  * RolloutBuffer.compute_returns_and_advantage (stable-baselines3 >= 2.0,
@@ -439,8 +447,9 @@ int64_t salp_state_ptr(SalpEnv* h);
  * tick's shared-reciprocal division, 12-13 sin and cos of the tick's yaw
  * function, 14-17 sin x, cos x, sin y, cos y of the tick's roll / pitch pair
  * function at (x, y), 18-20 the tick's world-frame rotation of (y, x, 1) by
- * the angles (x, y, x + y)}, x, y [n]; out [SALP_MATH_SELFTEST_ROWS][n]. */
-#define SALP_MATH_SELFTEST_ROWS 21
+ * the angles (x, y, x + y), 21 atan (select form), 22 atan (fdlibm's branches)},
+ * x, y [n]; out [SALP_MATH_SELFTEST_ROWS][n]. */
+#define SALP_MATH_SELFTEST_ROWS 23
 int salp_math_selftest(const double* x, const double* y, int64_t n, double* out, void* stream);
 
 /* State fields.  Names follow the reference attribute they hold. */

@@ -1663,6 +1663,8 @@ void oracle_math_selftest(const double* x, const double* y, int64_t n, double* o
         out[18 * n + i] = wf[0];
         out[19 * n + i] = wf[1];
         out[20 * n + i] = wf[2];
+        out[21 * n + i] = sm_atan(x[i]);
+        out[22 * n + i] = sm_atan_ref(x[i]);
     }
 }
 

@@ -206,6 +206,27 @@ def test_salp_robot_env_robot_views_and_recording():
     env.close()
 
 
+def test_task_attributes_write_through_only_by_assignment():
+    """target_point / obstacles: whole assignments reach the device state;
+    the getters hand out read-only copies, so an in-place edit raises instead
+    of changing a host copy the simulation never reads."""
+    env = _make_env()
+    assert len(env.obstacles) == env.num_obstacles
+    with pytest.raises(ValueError):
+        env.obstacles[0][0] = 1.0
+    with pytest.raises(AttributeError):
+        env.obstacles.append(np.zeros(2))
+    with pytest.raises(ValueError):
+        env.target_point[0] = 1.0
+    env.obstacles = [np.array([1.25, -0.5], np.float32)]
+    env.target_point = np.array([-1.0, 0.75], np.float32)
+    assert float(env._sim.field("n_obst")[0]) == 1.0
+    assert float(env._sim.field("obst0")[0]) == 1.25 and float(env._sim.field("obst1")[0]) == -0.5
+    assert float(env._sim.field("target0")[0]) == -1.0 and float(env._sim.field("target1")[0]) == 0.75
+    assert np.array_equal(env.obstacles[0], [1.25, -0.5])
+    env.close()
+
+
 def test_standalone_robot_class_matches_fixture():
     """compare_trajectories.simulate_trajectory's call sequence on the drop-in
     Robot (Python-float controls), record=True."""

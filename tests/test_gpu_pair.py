@@ -26,6 +26,17 @@ from oracle.sampled import _bits_differ
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def no_pair_timeouts():
+    """Every pair launch of the test met its partner wave on every tick: no
+    wait gave up (salp_pair_timeouts, read and cleared; process-wide)."""
+    probe = BatchedSalpEnv(64, seed=0)
+    probe.pair_timeouts()
+    yield
+    assert probe.pair_timeouts() == 0
+    probe.close()
+
+
 def _np(t):
     return t.detach().cpu().numpy()
 

@@ -143,17 +143,17 @@ def test_fused_step_equals_torch_clip_and_adam():
 @pytest.mark.parametrize("max_mb", [1024, 3])
 def test_fused_graph_is_kept_and_equals_eager(max_mb):
     """PPO with the fused step on one GPU replays one graph per epoch (or, with
-    max_graph_minibatches 3, a graph of 2 of the epoch's 8 minibatches four
-    times), captured in the first update and kept for every later one; three
-    iterations leave exactly (bit for bit: no atomics) the parameters, Adam
-    state and losses of the same learner stepping every minibatch eagerly, and
-    stay finite."""
+    max_graph_minibatches 3, a graph of 3 of the epoch's 8 minibatches twice
+    and a graph of the last 2), captured in the first update and kept for
+    every later one; three iterations leave exactly (bit for bit: no atomics)
+    the parameters, Adam state and losses of the same learner stepping every
+    minibatch eagerly, and stay finite."""
     out = []
     for graphs in (True, False):
         env = SalpVecEnv(32768, seed=0, infos=False)
         model = PPO("MlpPolicy", env, n_steps=8, batch_size=32768, n_epochs=2, seed=0, use_graphs=graphs,
                     max_graph_minibatches=max_mb)
-        assert model._graph_chunk(8) == (8 if max_mb >= 8 else 2)
+        assert model._graph_chunk(8) == min(8, max_mb)
         assert model.fused_update and model.use_graphs == graphs
         ids = []
         for _ in range(3):
@@ -161,6 +161,7 @@ def test_fused_graph_is_kept_and_equals_eager(max_mb):
             ids.append(id(model._epoch_graph))
         if graphs:
             assert model._epoch_graph is not None and len(set(ids)) == 1, "one epoch graph, kept across updates"
+            assert (model._rem_graph is not None) == (8 % min(8, max_mb) != 0)
         out.append(([t.detach().clone() for t in model._mlp_tensors] + [model._f_m.clone(), model._f_v.clone(),
                                                                         model._f_step.clone()],
                     [(r["pg_loss"], r["vf_loss"]) for r in model.history]))

@@ -172,3 +172,19 @@ def test_tick_world_frame_rotation():
         norm = float(mpmath.norm(v))
         for r in range(3):
             assert abs(out[18 + r][j] - float(want[r])) <= 4 * np.spacing(norm), (j, r)
+
+
+def test_select_form_atan_equals_fdlibm_branches():
+    """sm_atan (every range by selects, one division) equals fdlibm's branchy
+    sm_atan_ref bit for bit: every range, its boundaries, tiny, huge, signed
+    zeros, infinities and NaN."""
+    rng = np.random.default_rng(6)
+    edges = np.array([0.4375, 0.6875, 1.1875, 2.4375, 2.0 ** -27, 2.0 ** 66])
+    near = np.concatenate([np.nextafter(edges, 0), edges, np.nextafter(edges, np.inf)])
+    x = np.concatenate([rng.uniform(-4, 4, 20000), 10.0 ** rng.uniform(-320, 300, 20000),
+                        -(10.0 ** rng.uniform(-320, 300, 5000)), near, -near,
+                        [0.0, -0.0, np.inf, -np.inf, np.nan, 1.0, -1.0]])
+    out = oracle.math_selftest(x, np.ones_like(x))
+    a, b = out[21], out[22]
+    same = (a.view(np.int64) == b.view(np.int64)) | (np.isnan(a) & np.isnan(b))
+    assert same.all(), x[~same][:5]

@@ -8,7 +8,7 @@ OUT=${OUT:-gpurun_out/headline_ab.txt}
 for r in $(seq ${ROUNDS:-2}); do
     for lib in ${LIBS:-product}; do
         l=$lib; [ "$lib" = product ] && l=""
-        v=$(SALP_LIB=$l timeout -k 10 300 python bench.py --no-cpu-baseline --no-lockstep --no-parity-check --no-ppo \
+        v=$(SALP_AB_OLD_ABI=1 SALP_LIB=$l timeout -k 10 300 python bench.py --no-cpu-baseline --no-lockstep --no-parity-check --no-ppo \
             2>/dev/null | grep '^{' | python -c "import json,sys; d=json.load(sys.stdin); print(round(d['value']/1e6,2), round(d['kernel_ms_per_launch'],3))") || exit 1
         echo "$lib $v" >> "$OUT"
     done

@@ -32,7 +32,7 @@ def main():
                     help="mangled-name fragment of the counted instance (fingerprint)")
     ap.add_argument("--n-envs", type=int, default=65536)
     ap.add_argument("--tick-budget", type=int, default=8192)
-    ap.add_argument("--chunk", type=int, default=128)
+    ap.add_argument("--chunk", type=int, default=64)
     a = ap.parse_args()
     per = {}
     for path in sorted(glob.glob(os.path.join(ROOT, "gpurun_out", f"pmc_{a.tag}_*", "run_counter_collection.csv"))):
