@@ -240,11 +240,21 @@ def ppo_leg(a, rank, world, dev):
     from tools.bench_ppo import gae_roofline
     n, T = a.ppo_envs, a.ppo_steps
     env = SalpVecEnv(n, seed=a.seed, env_id_offset=env_id_offset(rank, n), device=dev.index, infos=False)
-    model = PPO("MlpPolicy", env, n_steps=T, batch_size=32768, n_epochs=10, seed=a.seed, collect="auto")
+    # SALP_BENCH_PPO_GRAPHS=0: eager update (tools/gpu_pmc_collect.sh: rocprofv3's counter collection does
+    # not survive the update's HIP graphs; eager and graphed updates are equal bit for bit, so the
+    # collection profiled is the same)
+    graphs = os.environ.get("SALP_BENCH_PPO_GRAPHS", "1") != "0"
+    model = PPO("MlpPolicy", env, n_steps=T, batch_size=32768, n_epochs=10, seed=a.seed, collect="auto",
+                use_graphs=graphs)
     model.learn(T * n)   # warm-up iteration
     for k in model.timing:
         model.timing[k] = 0.0
     torch.cuda.synchronize()
+    # the timed collection's starting point, for the sampled replay after it
+    check = rank == 0 and not a.no_parity_check and model.collect == "chained"
+    if check:
+        state0 = model.sim.get_state().cpu().numpy()
+        obs0 = model._obs.detach().cpu().numpy()
     if world > 1:
         dist.barrier()
     model.num_timesteps = 0
@@ -253,17 +263,95 @@ def ppo_leg(a, rank, world, dev):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     el_max, steps, _, _ = reduce_run(el, model.num_timesteps, 0.0, 0.0, device=dev)
+    collect_parity = None
+    if check:
+        # Parity of the timed collection (the checker, after the timed region):
+        # blocks of env ids replayed on the C oracle from their state before the
+        # call with the clipped actions the kernel recorded (oracle/sampled.py)
+        from grasp_lab_salp_amd.ppo import DIVERGED_OBS_ABS, DIVERGED_REWARD_ABS
+        from oracle import sampled
+        t_chk = time.perf_counter()
+        b = model.buf
+        collect_parity = sampled.check_collect(
+            state0, obs0, {k: getattr(b, k).detach().cpu().numpy() for k in ("obs", "actions", "rewards",
+                                                                             "episode_starts")},
+            model._last_obs.detach().cpu().numpy(), model.sim.get_state().cpu().numpy(), default_params(), a.seed,
+            env_offset=env_id_offset(rank, n),
+            guard=(DIVERGED_OBS_ABS, DIVERGED_REWARD_ABS) if model.reset_nonfinite else None)
+        collect_parity["seconds"] = time.perf_counter() - t_chk
+        collect_parity["what"] = ("the timed salp_collect: blocks of 64 env ids (first, last, one random) replayed "
+                                  "on the C oracle with the recorded clipped actions and the divergence guard; "
+                                  "observations, rewards (no-bootstrap rows), episode starts, final obs and state "
+                                  "bit for bit")
     gae = gae_roofline(T, n)
     timing = {k: reduce_run(v, 0, 0.0, 0.0, device=dev)[0] for k, v in model.timing.items()}
     env.close()
     del model, env
     torch.cuda.empty_cache()
-    return {"metric": "PPO env-steps/sec (collection + GAE + update), BASELINE configs[4]", "value": steps / el_max,
+    out = {"metric": "PPO env-steps/sec (collection + GAE + update), BASELINE configs[4]", "value": steps / el_max,
             "unit": "env-steps/s", "n_envs_per_gpu": n, "n_steps": T, "batch_size": 32768, "n_epochs": 10,
             "collect": "chained (salp_collect)" if T >= 256 else "lockstep (salp_step)",
             "iteration_s": el_max, "timing_s_max_over_ranks": timing,
             "gae_kernel": gae, "policy": "SB3 MlpPolicy 64-64 tanh (the reference's LSTM-256 RecurrentPPO: "
                                          "grasp_lab_salp_amd.recurrent_ppo, tools/bench_ppo.py --recurrent)"}
+    if collect_parity is not None:
+        out["collect_parity_sampled"] = collect_parity
+    out["collect_roofline_valu"] = collect_roofline(n, T, timing.get("collect_s"), collect_parity)
+    return out
+
+
+def collect_roofline(n, T, collect_s, parity):
+    """fp64 VALU roofline of the timed collection (the pair kernel
+    k_rollout_pair<true> at config 5's 32 768 envs): algorithmic flops
+    (F_TICK_ALGO per physics tick, the ticks measured by the collection's
+    sampled replay) and, from a committed PMC summary of this config whose
+    kernel fingerprint matches the library's, executed flops; both over the
+    timed collection phase (HIP events: the kernel plus the bootstrap value
+    GEMM)."""
+    import glob
+    from grasp_lab_salp_amd import _codeobj
+    from grasp_lab_salp_amd._lib import LIB_PATH
+    if not collect_s:
+        return None
+    tps = parity["ticks_per_env_step"] if parity else None
+    res = {"bound": "fp64-valu", "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s", "kernel": "k_rollout_pair<true>",
+           "collect_s": collect_s, "ticks_per_env_step": tps}
+    if tps:
+        fl = F_TICK_ALGO * n * T * tps / collect_s / 1e12
+        res.update({"achieved": fl, "frac": fl / FP64_VALU_PEAK_TFLOPS, "count": "algorithmic (F_TICK_ALGO x "
+                    "measured ticks of the replayed env-steps)"})
+    sha = _codeobj.kernel_sha(LIB_PATH, _codeobj.PAIR_COLLECT_KERNEL)
+    res["kernel_sha16"] = sha
+    best, stale = None, []
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_collect_summary.json"))):
+        try:
+            s = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if s.get("config") == {"n_envs": n, "n_steps": T} and s.get("derived", {}).get("fp64_flops_per_executed_tick"):
+            if s.get("kernel_sha16") == sha:
+                best = (os.path.basename(path), s)
+            else:
+                stale.append(os.path.basename(path))
+    if best is None:
+        res["executed"] = None
+        res["executed_reason"] = (f"no PMC summary of this collection measured on this build (kernel_sha16 {sha}); "
+                                  f"stale: {stale[-2:]}" if stale else "no PMC summary of this collection")
+    elif tps:
+        # the probe's executed fp64 flops per physics tick (its own collection, replayed for its
+        # ticks) times this collection's ticks
+        d = best[1]["derived"]
+        ex = d["fp64_flops_per_executed_tick"] * n * T * tps / collect_s / 1e12
+        res["executed"] = {"achieved": ex, "frac": ex / FP64_VALU_PEAK_TFLOPS, "source": best[0],
+                           "fp64_flops_per_executed_tick": d["fp64_flops_per_executed_tick"],
+                           "hbm_bytes_per_dispatch": d.get("hbm_bytes"), "active_valu_frac": d.get("active_valu_frac"),
+                           "note": "PMC of tools/collect_pmc_probe.py (the same kernel, size and chunk, a fresh "
+                                   "policy): fp64 VALU instructions x 64 lanes (FMA = 2) per executed tick, times "
+                                   "the timed collection's measured ticks, over its collect phase"}
+    else:
+        res["executed"] = None
+        res["executed_reason"] = "no measured ticks (the collection's sampled replay did not run)"
+    return res
 
 
 def dry_run(a, world, rank):

@@ -124,3 +124,5 @@ def kernel_sha(lib_path, contains):
 
 # The bench's dominant kernel: k_rollout<RAND = false, POL = false>.
 ROLLOUT_KERNEL = "k_rolloutILb0ELb0EE"
+# The PPO leg's collection kernel (config 5, 32 768 envs): k_rollout_pair<POL = true>.
+PAIR_COLLECT_KERNEL = "k_rollout_pairILb1EE"

@@ -1592,16 +1592,16 @@ int32_t rollout_steady_q8() {
     return q;
 }
 // The same budget for k_rollout_pair, whose steady ticks cost relatively more
-// (the per-tick packet exchange is the same for every kind of tick): q = 320
-// (32 768 envs, profiles/r4_experiments.md r4h / r4q / r4x: 256-480 x chunk
-// 96-512; with salp_collect's chunk 192 the bench's PPO collection takes
-// 0.363-0.365 s at 320 against 0.365-0.367 s at 352, whose random-policy
-// collect_bench rate is 1 % higher).  SALP_PAIR_STEADY_Q8 overrides it.
+// (the per-tick packet exchange is the same for every kind of tick): q = 320 in
+// round 4 (32 768 envs, profiles/r4_experiments.md r4h / r4q / r4x); round 5's
+// cheaper settled tick: q = 400 (320 / 360 / 400 / 440 / 480 x chunk 96-256,
+// collect_bench at 32 768 envs 25.4 -> 26.3-26.7 M at chunk 192,
+// profiles/r5_experiments.md r5n-r5o).  SALP_PAIR_STEADY_Q8 overrides it.
 int32_t pair_steady_q8() {
     static const int32_t q = [] {
         const char* e = std::getenv("SALP_PAIR_STEADY_Q8");
         const long v = e ? std::strtol(e, nullptr, 10) : 0;
-        return (int32_t)(v > 0 && v < (1 << 16) ? v : 320);
+        return (int32_t)(v > 0 && v < (1 << 16) ? v : 400);
     }();
     return q;
 }

@@ -125,3 +125,71 @@ def check(state, steps_done, buffers, params, seed, env_offset=0, ids=None, thre
         res["buffer_row_mismatches"] = mism
     res["ok"] = res["state_mismatch_envs"] == 0 and res.get("buffer_row_mismatches", 0) == 0
     return res
+
+
+def check_collect(state0, obs0, bufs, last_obs, state1, params, seed, env_offset=0, block=64, n_random_blocks=1,
+                  guard=(1e3, 1e4), rng_seed=0):
+    """Sampled parity check of one salp_collect call (the PPO collection,
+    src/train_robot_recurrent_ppo.py:85-107 with SB3's collect_rollouts).
+    Blocks of `block` consecutive env ids (the first, the last and
+    `n_random_blocks` random aligned ones) are replayed on the C oracle from
+    their state before the call (state0 [NUM_FIELDS, n], obs0 [n, obs_dim]),
+    stepping with the clipped actions the kernel recorded and resetting where
+    the learner's divergence guard (guard = (obs_abs, reward_abs); None: off)
+    fired, the guard re-evaluated on the oracle's outputs.  The recorded
+    observations, rewards (rows without a timeout bootstrap, whose value term
+    is the policy's), episode starts, the final observations and the final
+    state must equal the oracle's bit for bit (NaN payloads and signed zeros
+    aside, as check()).  Also returns the physics ticks of the replayed
+    env-steps (the collection's measured cycle length)."""
+    n = state0.shape[1]
+    T = bufs["obs"].shape[0]
+    rng = np.random.default_rng(rng_seed)
+    starts = {0, max(n - block, 0)}
+    for _ in range(n_random_blocks):
+        starts.add(int(rng.integers(0, max(n // block, 1))) * block)
+    low, high = np.float32([0, 0, -1]), np.float32([1, 1, 1])
+    res = {"envs_checked": 0, "env_steps_replayed": 0, "ticks_replayed": 0, "obs_row_mismatches": 0,
+           "reward_mismatches": 0, "episode_start_mismatches": 0, "bootstrap_rows_skipped": 0,
+           "guard_resets": 0, "last_obs_mismatches": 0, "state_mismatch_envs": 0, "blocks": sorted(starts)}
+    for b0 in sorted(starts):
+        ids = np.arange(b0, min(b0 + block, n))
+        m = len(ids)
+        o = orc.Oracle(params, m, seed=seed, env_offset=env_offset + b0)
+        o.state[:] = state0[:, ids]
+        obs = np.array(obs0[ids], np.float32)
+        for t in range(T):
+            res["obs_row_mismatches"] += int(_bits_differ(bufs["obs"][t][ids], obs).any(-1).sum())
+            a = np.clip(bufs["actions"][t][ids], low, high)
+            r = o.step(a, auto_reset=True)
+            res["ticks_replayed"] += int(r["ticks"].sum())
+            term, trunc = r["terminated"].astype(bool), r["truncated"].astype(bool)
+            done = term | trunc
+            last = np.where(done[:, None], r["terminal_obs"], r["obs"])
+            if guard is not None:
+                bad = ~(np.abs(r["reward"]) <= guard[1]) | ~np.all(np.abs(last) <= guard[0], axis=1)
+            else:
+                bad = np.zeros(m, bool)
+            got = bufs["rewards"][t][ids]
+            boot = trunc & ~term & ~bad
+            res["bootstrap_rows_skipped"] += int(boot.sum())
+            want = np.where(bad, np.float32(0), r["reward"].astype(np.float32))
+            res["reward_mismatches"] += int((_bits_differ(got, want) & ~boot).sum())
+            fresh_mask = bad & ~done
+            res["guard_resets"] += int(bad.sum())
+            if fresh_mask.any():
+                fresh = o.reset(fresh_mask.astype(np.uint8))
+                obs = np.where(fresh_mask[:, None], fresh, r["obs"])
+            else:
+                obs = r["obs"]
+            if t + 1 < T:
+                want_start = (done | bad).astype(np.float32)
+                res["episode_start_mismatches"] += int((bufs["episode_starts"][t + 1][ids] != want_start).sum())
+        res["last_obs_mismatches"] += int(_bits_differ(last_obs[ids], obs).any(-1).sum())
+        res["state_mismatch_envs"] += int(_bits_differ(state1[:, ids], o.state).any(0).sum())
+        res["envs_checked"] += m
+        res["env_steps_replayed"] += m * T
+    res["ticks_per_env_step"] = res["ticks_replayed"] / max(res["env_steps_replayed"], 1)
+    res["ok"] = not any(res[k] for k in ("obs_row_mismatches", "reward_mismatches", "episode_start_mismatches",
+                                         "last_obs_mismatches", "state_mismatch_envs"))
+    return res

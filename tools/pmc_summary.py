@@ -33,6 +33,12 @@ def main():
     ap.add_argument("--n-envs", type=int, default=65536)
     ap.add_argument("--tick-budget", type=int, default=8192)
     ap.add_argument("--chunk", type=int, default=64)
+    ap.add_argument("--config-json", help="the run's config as JSON instead of n_envs / tick_budget / chunk "
+                                         "(e.g. the PPO collection: {\"n_envs\": 32768, \"n_steps\": 256})")
+    ap.add_argument("--suffix", default="pmc_summary", help="output profiles/<tag>_<suffix>.json")
+    ap.add_argument("--command", help="the profiled command, for the record")
+    ap.add_argument("--workload-json", help="a JSON file the profiled program wrote about its workload "
+                                           "(tools/collect_pmc_probe.py: env-steps per dispatch, ticks per env-step)")
     a = ap.parse_args()
     per = {}
     for path in sorted(glob.glob(os.path.join(ROOT, "gpurun_out", f"pmc_{a.tag}_*", "run_counter_collection.csv"))):
@@ -47,13 +53,17 @@ def main():
     if not per:
         raise SystemExit(f"no counters for {a.kernel} under gpurun_out/pmc_{a.tag}_*")
     g = lambda k: per[k]["mean"] if k in per else None  # noqa: E731
-    out = {"tag": a.tag, "kernel": a.kernel,
-           "config": {"n_envs": a.n_envs, "tick_budget": a.tick_budget, "chunk": a.chunk},
-           "command": "tools/gpu_pmc.sh: rocprofv3 --pmc <group> --kernel-trace -- python3 bench.py "
-                      "--steps 2 --warmup 1 --no-cpu-baseline --no-lockstep --no-parity-check --no-ppo, one pass per group",
+    config = (json.loads(a.config_json) if a.config_json else
+              {"n_envs": a.n_envs, "tick_budget": a.tick_budget, "chunk": a.chunk})
+    out = {"tag": a.tag, "kernel": a.kernel, "config": config,
+           "command": a.command or ("tools/gpu_pmc.sh: rocprofv3 --pmc <group> --kernel-trace -- python3 bench.py "
+                                    "--steps 2 --warmup 1 --no-cpu-baseline --no-lockstep --no-parity-check --no-ppo, "
+                                    "one pass per group"),
            "kernel_symbol": a.symbol,
            "kernel_sha16": _codeobj.kernel_sha(os.path.join(ROOT, "grasp_lab_salp_amd", "libsalp.so"), a.symbol),
            "per_dispatch": per, "derived": {}}
+    if a.workload_json:
+        out["workload"] = json.load(open(a.workload_json))
     d = out["derived"]
     if g("FETCH_SIZE") is not None:
         d["fetch_bytes"] = g("FETCH_SIZE") * 1024 * 2
@@ -66,12 +76,18 @@ def main():
     if None not in f64:
         d["fp64_valu_insts"] = sum(f64)
         d["fp64_flops"] = 64 * (f64[0] + f64[1] + 2 * f64[2] + f64[3])
-        d["fp64_flops_per_env_tick"] = d["fp64_flops"] / (a.n_envs * a.tick_budget)
+        if not a.config_json:
+            # per budget tick (n_envs x tick_budget): round 4's normalisation; bench.py
+            # reports flops per executed tick from the measured ticks per env-step
+            d["fp64_flops_per_env_tick"] = d["fp64_flops"] / (a.n_envs * a.tick_budget)
+    wl = out.get("workload", {})
+    if "fp64_flops" in d and wl.get("env_steps_per_dispatch") and wl.get("ticks_per_env_step"):
+        d["fp64_flops_per_executed_tick"] = d["fp64_flops"] / (wl["env_steps_per_dispatch"] * wl["ticks_per_env_step"])
     if g("SQ_WAVES"):
         d["valu_insts_per_wave"] = g("SQ_INSTS_VALU") / g("SQ_WAVES")
         d["wait_any_frac"] = g("SQ_WAIT_ANY") / g("SQ_WAVE_CYCLES")
         d["active_valu_frac"] = g("SQ_ACTIVE_INST_VALU") / g("SQ_WAVE_CYCLES")
-    dst = os.path.join(ROOT, "profiles", f"{a.tag}_pmc_summary.json")
+    dst = os.path.join(ROOT, "profiles", f"{a.tag}_{a.suffix}.json")
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(d, indent=1))
 
