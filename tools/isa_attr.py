@@ -81,6 +81,111 @@ def loops(ins):
     return sorted(set(out), key=lambda r: r[1] - r[0])
 
 
+def natural_loops(ins):
+    """Natural loops of the kernel's control-flow graph: for every loop header
+    (the target of a back edge: an edge to a block that dominates its source),
+    the header plus every basic block that reaches one of its back edges
+    without passing through it.  Unlike an
+    address range, this includes the blocks the compiler laid out after the
+    loop's back edge (cold paths, a branch's else side).  Returns
+    [(header_addr, [instruction addresses])]."""
+    addrs = [x[0] for x in ins]
+    index = {a: k for k, a in enumerate(addrs)}
+    def target(addr, op, args):
+        m = re.match(r"(-?\d+)", args)
+        if not (op.startswith("s_cbranch") or op == "s_branch") or not m:
+            return None
+        off = int(m.group(1))
+        if off >= 32768:
+            off -= 65536
+        return addr + 4 + 4 * off
+    # basic block leaders
+    leaders = {addrs[0]}
+    for k, (addr, op, args) in enumerate(ins):
+        t = target(addr, op, args)
+        if t is not None:
+            leaders.add(t)
+            if k + 1 < len(ins):
+                leaders.add(addrs[k + 1])
+        elif op in ("s_endpgm", "s_setpc_b64") and k + 1 < len(ins):
+            leaders.add(addrs[k + 1])
+    starts = sorted(a for a in leaders if a in index)
+    blocks = {}
+    for j, a in enumerate(starts):
+        end = starts[j + 1] if j + 1 < len(starts) else addrs[-1] + 4
+        blocks[a] = [x for x in addrs[index[a]:] if x < end]
+    succ = {a: [] for a in blocks}
+    for a, body in blocks.items():
+        last = body[-1]
+        _, op, args = ins[index[last]]
+        t = target(last, op, args)
+        nxt = addrs[index[last] + 1] if index[last] + 1 < len(addrs) else None
+        if t is not None and t in blocks:
+            succ[a].append(t)
+        if op not in ("s_branch", "s_endpgm", "s_setpc_b64") and nxt is not None and nxt in blocks:
+            succ[a].append(nxt)
+    pred = {a: [] for a in blocks}
+    for a, ss in succ.items():
+        for b in ss:
+            pred[b].append(a)
+    # dominators (Cooper, Harvey & Kennedy's iterative algorithm) over the
+    # blocks reachable from the entry, in reverse postorder
+    entry = starts[0]
+    order, seen, stack = [], {entry}, [(entry, iter(succ[entry]))]
+    while stack:
+        node, it = stack[-1]
+        nxt = next(it, None)
+        if nxt is None:
+            order.append(node)
+            stack.pop()
+        elif nxt not in seen:
+            seen.add(nxt)
+            stack.append((nxt, iter(succ[nxt])))
+    rpo = order[::-1]
+    num = {b: k for k, b in enumerate(rpo)}
+    idom = {entry: entry}
+    changed = True
+    while changed:
+        changed = False
+        for b in rpo[1:]:
+            ps = [p for p in pred[b] if p in idom]
+            if not ps:
+                continue
+            new_idom = ps[0]
+            for p in ps[1:]:
+                x, y = p, new_idom
+                while x != y:
+                    while num[x] > num[y]:
+                        x = idom[x]
+                    while num[y] > num[x]:
+                        y = idom[y]
+                new_idom = x
+            if idom.get(b) != new_idom:
+                idom[b] = new_idom
+                changed = True
+
+    def dominates(h, b):
+        while True:
+            if b == h:
+                return True
+            if b == entry or b not in idom:
+                return False
+            b = idom[b]
+
+    loops_ = {}
+    for a, ss in succ.items():
+        for h in ss:
+            if a in idom and dominates(h, a):   # back edge a -> h
+                body = loops_.setdefault(h, {h})
+                stack = [a]
+                while stack:
+                    x = stack.pop()
+                    if x not in body:
+                        body.add(x)
+                        stack.extend(pred[x])
+    return [(h, sorted(i for b in body for i in blocks[b])) for h, body in loops_.items()]
+
+
 def symbolize(dev, addrs):
     p = subprocess.run([f"{LLVM}/llvm-symbolizer", f"--obj={dev}", "--inlining", "--relative-address"],
                        input="\n".join(hex(a) for a in addrs), capture_output=True, text=True, check=True)
@@ -150,17 +255,17 @@ def main():
     ap.add_argument("--min-loop", type=int, default=300, help="smallest loop (instructions) to report")
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--max-loop", type=int, default=2500, help="largest natural loop to report")
     a = ap.parse_args()
     dev = build(a.force)
     ins = disasm(dev, a.kernel)
     marks = device_part_table()
     by_addr = {x[0]: x for x in ins}
-    reported = []
-    for lo, hi in loops(ins):
-        body = [x for x in ins if lo <= x[0] <= hi]
-        if len(body) < a.min_loop or any(lo <= r0 and r1 <= hi for r0, r1 in reported):
+    for h, members in sorted(natural_loops(ins), key=lambda x: len(x[1])):
+        if not a.min_loop <= len(members) <= a.max_loop:
             continue
-        reported.append((lo, hi))
+        body = [by_addr[m] for m in members]
+        lo, hi = members[0], members[-1]
         frames = symbolize(dev, [x[0] for x in body])
         cls = collections.Counter(classify(op) for _, op, _ in body)
         parts = collections.Counter()
@@ -174,7 +279,7 @@ def main():
                 parts_f64[part] += 1
             if routine:
                 routines[routine] += 1
-        print(f"== loop {lo:#x}..{hi:#x}: {len(body)} instructions  " +
+        print(f"== natural loop, header {h:#x} (span {lo:#x}..{hi:#x}): {len(body)} instructions  " +
               "  ".join(f"{k} {v}" for k, v in sorted(cls.items())))
         print("   by part (all / fp64):")
         for k, v in parts.most_common(a.top):
@@ -183,7 +288,6 @@ def main():
         for k, v in routines.most_common(12):
             print(f"     {v:5d}  {k}")
         print("   top opcodes:", ", ".join(f"{k} {v}" for k, v in ops.most_common(16)))
-    _ = by_addr
 
 
 if __name__ == "__main__":
