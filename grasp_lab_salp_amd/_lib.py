@@ -129,6 +129,7 @@ SIGNATURES = {
     "salp_lstm_step_backward": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32] + [_V] * 11),
     "salp_set_lockstep_order": (ctypes.c_int, [_H, ctypes.c_int]),
     "salp_set_rollout_kernel": (ctypes.c_int, [_H, ctypes.c_int]),
+    "salp_set_step_kernel": (ctypes.c_int, [_H, ctypes.c_int]),
     "salp_pair_timeouts": (ctypes.c_int, [_H, ctypes.POINTER(ctypes.c_uint64), _V]),
     "salp_robot_reset": (ctypes.c_int, [_H, _V, _V]),
     "salp_nozzle_set_angles": (ctypes.c_int, [_H, _V, _V]),

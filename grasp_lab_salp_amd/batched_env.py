@@ -193,6 +193,14 @@ class BatchedSalpEnv:
         identical in every mode."""
         self._check(_lib.load().salp_set_rollout_kernel(self._h, int(mode)))
 
+    def set_step_kernel(self, mode):
+        """Kernel of :meth:`step` (salp_set_step_kernel): 1 = one env per wave
+        (k_step_wave: the geometry of 64 ticks at once, then their dynamics),
+        0 = one env per lane (k_step), -1 = one env per wave up to 1 024 envs
+        (default).  Recording always uses k_step.  Results are identical in
+        every mode."""
+        self._check(_lib.load().salp_set_step_kernel(self._h, int(mode)))
+
     def pair_timeouts(self):
         """Partner waits of the two-wave kernel that gave up since the last
         call (salp_pair_timeouts; synchronises the stream).  Nonzero means some

@@ -656,6 +656,185 @@ SD bool next_tick_steady(const Hot& h, const Params& P) {
     return h.ct > 0.0 && h.L == P.L0 && h.W == P.W0 && !h.g32 && ct > h.b1 && ct > h.mx;
 }
 
+/* The dynamics of one tick (src/robot.py:854-875: _newton_equations,
+ * _euler_equations, _update_motion_states) on the geometry the lane holds
+ * (h.geo, centre of mass and its rates, phase, width): everything of Robot.step
+ * before cycle_time / update_state / update_properties, in three parts (PARTS
+ * bits): TD_FORCES the forces and the velocity integration, TD_KINEMATICS the
+ * Euler-angle rates at the current angles, the new angles, their sin / cos
+ * (kept for the next tick) and the world-frame velocity into the world
+ * position, TD_POSITIONS the body-frame position and angle.  The forces never
+ * read the angles or the world position, so the kinematics only follow them
+ * (k_step_wave runs them on a second wave).  SETTLED: see tick. */
+enum { TD_FORCES = 1, TD_KINEMATICS = 2, TD_POSITIONS = 4, TD_ALL = 7 };
+template <bool REC, bool RAND, bool SETTLED, int PARTS = TD_ALL>
+SD void tick_dynamics(Hot& h, const Params& P, double* rec, int64_t rs) {
+    if (PARTS & TD_FORCES) {
+        const Geo& g = h.geo;
+        const double m = g.m;
+        /* coefficients of this cycle: the reference's means, or (RAND) the
+         * Robot._randomize_parameters draw of set_control */
+        const double cd = RAND ? h.rnd.cd : CD, dfr = RAND ? h.rnd.dfr : DRAG_FORCE_RATIO,
+                     dtr = RAND ? h.rnd.dtr : DRAG_TORQUE_RATIO;
+        const double cam0 = RAND ? h.rnd.amf0 : AMF0, cam1 = RAND ? h.rnd.amf1 : AMF1,
+                     cam2 = RAND ? h.rnd.amf2 : AMF2;
+        const double car0 = RAND ? h.rnd.amrf0 : AMRF, car1 = RAND ? h.rnd.amrf1 : AMRF,
+                     car2 = RAND ? h.rnd.amrf2 : AMRF;
+        const double cat0 = RAND ? h.rnd.amt0 : AMT0, cat1 = RAND ? h.rnd.amt1 : AMT1,
+                     cat2 = RAND ? h.rnd.amt2 : AMT2;
+        /* OUDisturbance.sample (src/robot.py:233-242) of the force (x, y kept) and
+         * torque (z kept) processes, src/robot.py:796-800, 834-838 */
+        double nf0 = 0.0, nf1 = 0.0, nt2 = 0.0;
+        if (RAND && P.rand_dist) {
+            double z0, z1, z2;
+            sr_normals3(P.seed, h.env_id, (uint64_t)h.rnd.tick, &z0, &z1, &z2);
+            h.rnd.tick += 1.0;
+            h.rnd.ouf0 = sr_ou_step(h.rnd.ouf0, SR_OU_FORCE_THETA, SR_OU_FORCE_SIGMA, z0);
+            h.rnd.ouf1 = sr_ou_step(h.rnd.ouf1, SR_OU_FORCE_THETA, SR_OU_FORCE_SIGMA, z1);
+            h.rnd.out2 = sr_ou_step(h.rnd.out2, SR_OU_TORQUE_THETA, SR_OU_TORQUE_SIGMA, z2);
+            nf0 = h.rnd.ouf0; nf1 = h.rnd.ouf1; nt2 = h.rnd.out2;
+        }
+        /* ---------------- Newton ---------------- */
+        /* Coriolis force -w x (M v)  (src/dynamics.py:159-162) */
+        double mv0 = m * h.v0, mv1 = m * h.v1, mv2 = m * h.v2;
+        double cf0 = -cross_c(h.w1, mv2, h.w2, mv1), cf1 = -cross_c(h.w2, mv0, h.w0, mv2),
+               cf2 = -cross_c(h.w0, mv1, h.w1, mv0);
+        /* drag force (src/dynamics.py:110-116); product mode: (k C v) (|v| + ratio) */
+        const double vnr = np_norm3(h.v0, h.v1, h.v2) + dfr;
+        double df0 = (g.kc0 * h.v0) * vnr;
+        double df1 = (g.kc1 * h.v1) * vnr;
+        double df2 = (g.kc1 * h.v2) * vnr;
+        /* jet force, JET phase only (src/robot.py:937-951, src/dynamics.py:87-101) */
+        const bool jet = !SETTLED && h.phase == JET;
+        double jf0 = jet ? g.mr * (h.d0 * g.speed) * -cd : 0.0;
+        double jf1 = jet ? g.mr * (h.d1 * g.speed) * -cd : 0.0;
+        double jf2 = jet ? g.mr * (h.d2 * g.speed) * -cd : 0.0;
+        /* added-mass force (src/dynamics.py:131-141) */
+        const double mr = SETTLED ? 0.0 : g.mr;
+        double am0 = m * cam0, am1 = m * cam1, am2 = m * cam2;
+        double amr0 = mr * car0, amr1 = mr * car1, amr2 = mr * car2;
+        double amv0 = am0 * h.v0, amv1 = am1 * h.v1, amv2 = am2 * h.v2;
+        double af0 = -sm_mad(amr0, h.v0, sm_mad(am0, h.a0, cross_c(h.w1, amv2, h.w2, amv1)));
+        double af1 = -sm_mad(amr1, h.v1, sm_mad(am1, h.a1, cross_c(h.w2, amv0, h.w0, amv2)));
+        double af2 = -sm_mad(amr2, h.v2, sm_mad(am2, h.a2, cross_c(h.w0, amv1, h.w1, amv0)));
+        /* fictitious forces of the moving center of mass (src/robot.py:806-810);
+         * com = (cx, 0, 0) */
+        const double cx = h.com, crx = SETTLED ? 0.0 : h.comr;
+        double acc_y = (h.w0 * (h.w1 * cx) + (h.w2 * crx) * 2.0) + h.al2 * cx;
+        double acc_z = (h.w0 * (h.w2 * cx) + -(h.w1 * crx) * 2.0) + -(h.al1 * cx);
+        double acc_x = cross_c(h.w1, -(h.w1 * cx), h.w2, h.w2 * cx) + (SETTLED ? 0.0 : h.coma);
+        /* total force and linear acceleration (src/dynamics.py:5-10) */
+        /* F * (1/m) (product mode; src/dynamics.py:5-10 solves diag(m) a = F) */
+        double na0, na1, na2;
+        const double rm = g.rm;
+        if (RAND) {   /* + force noise (z: zero) */
+            na0 = sm_mad(acc_x, m, (((jf0 + df0) + af0) + cf0) + nf0) * rm;
+            na1 = sm_mad(acc_y, m, (((jf1 + df1) + af1) + cf1) + nf1) * rm;
+            na2 = sm_mad(acc_z, m, (((jf2 + df2) + af2) + cf2) + 0.0) * rm;
+        } else {
+            na0 = sm_mad(acc_x, m, ((jf0 + df0) + af0) + cf0) * rm;
+            na1 = sm_mad(acc_y, m, ((jf1 + df1) + af1) + cf1) * rm;
+            na2 = sm_mad(acc_z, m, ((jf2 + df2) + af2) + cf2) * rm;
+        }
+        /* ---------------- Euler ---------------- */
+        const double I0 = g.I0, I1 = g.I1;
+        /* Coriolis torque -w x (I w) (src/dynamics.py:165-168) */
+        double iw0 = I0 * h.w0, iw1 = I1 * h.w1, iw2 = I1 * h.w2;
+        double ct0 = -cross_c(h.w1, iw2, h.w2, iw1), ct1 = -cross_c(h.w2, iw0, h.w0, iw2),
+               ct2 = -cross_c(h.w0, iw1, h.w1, iw0);
+        /* drag torque (src/dynamics.py:119-128); product mode: (C k A w) (|w| dims + width ratio) */
+        const double wn = np_norm3(h.w0, h.w1, h.w2), wr = h.W * dtr;
+        const double sx = sm_fma(wn, g.dimx, wr), sy = sm_fma(wn, g.dimy, wr);
+        double dt0 = (g.ra0 * h.w0) * sx;
+        double dt1 = (g.ra1 * h.w1) * sy;
+        double dt2 = (g.ra1 * h.w2) * sy;
+        /* jet torque r x F, r = (mid_x - L/2, 0, 0) (src/robot.py:931-935) */
+        double jt1 = -(g.rx * jf2), jt2 = g.rx * jf1;
+        /* deformation torque -(dI/dt) w; prev_I <- I (src/robot.py:888-896) */
+        double ir0 = 0.0, ir1 = 0.0, ir2 = 0.0;   /* settled: (I - prev_I) / dt = +0 / dt */
+        if (!SETTLED) {
+            ir0 = div_dt(I0 - h.pI0);
+            ir1 = div_dt(I1 - h.pI1);
+            ir2 = ir1;
+            if (h.pI2 != h.pI1) ir2 = div_dt(I1 - h.pI2);   /* prev_I[1,1] == prev_I[2,2] always */
+            h.pI0 = I0; h.pI1 = I1; h.pI2 = I1;
+        }
+        double dft0 = -(ir0 * h.w0), dft1 = -(ir1 * h.w1), dft2 = -(ir2 * h.w2);
+        /* added-mass torque, I_rate term identically zero (src/dynamics.py:144-156) */
+        double at0 = I0 * cat0, at1 = I1 * cat1, at2 = I1 * cat2;
+        double atw0 = at0 * h.w0, atw1 = at1 * h.w1, atw2 = at2 * h.w2;
+        double amt0 = -(sm_mad(at0, h.al0, cross_c(h.w1, atw2, h.w2, atw1)) + cross_c(h.v1, amv2, h.v2, amv1));
+        double amt1 = -(sm_mad(at1, h.al1, cross_c(h.w2, atw0, h.w0, atw2)) + cross_c(h.v2, amv0, h.v0, amv2));
+        double amt2 = -(sm_mad(at2, h.al2, cross_c(h.w0, atw1, h.w1, atw0)) + cross_c(h.v0, amv1, h.v1, amv0));
+        /* total torque and angular acceleration (src/dynamics.py:13-17) */
+        /* tau * (1/I) (product mode; src/dynamics.py:13-17) */
+        double nal0, nal1, nal2;
+        const double rI0 = g.rI0, rI1 = g.rI1;
+        if (RAND) {   /* + torque noise (x, y: zero) */
+            nal0 = ((sm_mad(-ir0, h.w0, dt0 + ct0) + amt0) + 0.0) * rI0;
+            nal1 = ((sm_mad(-ir1, h.w1, (jt1 + dt1) + ct1) + amt1) + 0.0) * rI1;
+            nal2 = ((sm_mad(-ir2, h.w2, (jt2 + dt2) + ct2) + amt2) + nt2) * rI1;
+        } else {
+            nal0 = (sm_mad(-ir0, h.w0, dt0 + ct0) + amt0) * rI0;
+            nal1 = (sm_mad(-ir1, h.w1, (jt1 + dt1) + ct1) + amt1) * rI1;
+            nal2 = (sm_mad(-ir2, h.w2, (jt2 + dt2) + ct2) + amt2) * rI1;
+        }
+        if (REC) {
+            const double z = 0.0;
+            auto put = [&](int col, double x) { rec[(int64_t)col * rs] = x; };
+            put(SALP_T_JETV0, jet ? h.d0 * g.speed : 0.0);
+            put(SALP_T_JETV1, jet ? h.d1 * g.speed : 0.0);
+            put(SALP_T_JETV2, jet ? h.d2 * g.speed : 0.0);
+            put(SALP_T_JETF0, jf0); put(SALP_T_JETF1, jf1); put(SALP_T_JETF2, jf2);
+            put(SALP_T_JETT0, z * jf2 - z * jf1); put(SALP_T_JETT1, jt1); put(SALP_T_JETT2, jt2);
+            put(SALP_T_DRAGF0, df0); put(SALP_T_DRAGF1, df1); put(SALP_T_DRAGF2, df2);
+            put(SALP_T_DRAGT0, dt0); put(SALP_T_DRAGT1, dt1); put(SALP_T_DRAGT2, dt2);
+            put(SALP_T_CORF0, cf0); put(SALP_T_CORF1, cf1); put(SALP_T_CORF2, cf2);
+            put(SALP_T_CORT0, ct0); put(SALP_T_CORT1, ct1); put(SALP_T_CORT2, ct2);
+            put(SALP_T_AMF0, af0); put(SALP_T_AMF1, af1); put(SALP_T_AMF2, af2);
+            put(SALP_T_AMT0, amt0); put(SALP_T_AMT1, amt1); put(SALP_T_AMT2, amt2);
+            put(SALP_T_DEFT0, dft0); put(SALP_T_DEFT1, dft1); put(SALP_T_DEFT2, dft2);
+            put(SALP_T_ACCF0, acc_x * m); put(SALP_T_ACCF1, acc_y * m); put(SALP_T_ACCF2, acc_z * m);
+        }
+        h.a0 = na0; h.a1 = na1; h.a2 = na2;
+        h.al0 = nal0; h.al1 = nal1; h.al2 = nal2;
+        /* ---------------- integrate (semi-implicit Euler) ---------------- */
+        h.v0 = sm_mad(na0, DT, h.v0); h.v1 = sm_mad(na1, DT, h.v1); h.v2 = sm_mad(na2, DT, h.v2);
+        h.w0 = sm_mad(nal0, DT, h.w0); h.w1 = sm_mad(nal1, DT, h.w1); h.w2 = sm_mad(nal2, DT, h.w2);
+    }
+    if (PARTS & TD_KINEMATICS) {
+        {   /* to_euler_angle_rate_jit (src/dynamics.py:20-31) at the current angles;
+             * product mode (the oracle's to_euler_angle_rate): u = sin(phi) w1 +
+             * cos(phi) w2, g = u / cos(theta) is row 2 and tan(theta) u = sin(theta) g
+             * row 0's tail */
+            const double u = sm_fma(h.cp, h.w2, h.sp * h.w1);
+            const double g2 = qdiv(u, rcp_of(h.cth));
+            double r0 = sm_fma(h.st, g2, h.w0);
+            double r1 = sm_fma(-h.sp, h.w2, h.cp * h.w1);
+            double r2 = g2;
+            h.e0 = sm_mad(r0, DT, h.e0); h.e1 = sm_mad(r1, DT, h.e1); h.e2 = sm_mad(r2, DT, h.e2);
+            if (REC) {
+                rec[(int64_t)SALP_T_ETAR0 * rs] = r0;
+                rec[(int64_t)SALP_T_ETAR1 * rs] = r1;
+                rec[(int64_t)SALP_T_ETAR2 * rs] = r2;
+            }
+        }
+        {   /* to_world_frame_jit (src/dynamics.py:34-58) at the new angles (world_frame;
+             * roll / pitch sin / cos kept for the next tick's Euler-rate map) */
+            double ss, cs;
+            sm_sincos_rp2(h.e0, h.e1, &h.sp, &h.cp, &h.st, &h.cth, P.sk);
+            sm_sincos_yaw_p(h.e2, &ss, &cs, P.sk);
+            double vw[3];
+            sm_world_frame(h.sp, h.cp, h.st, h.cth, ss, cs, h.v0, h.v1, h.v2, vw);
+            h.p0 = sm_mad(vw[0], DT, h.p0); h.p1 = sm_mad(vw[1], DT, h.p1); h.p2 = sm_mad(vw[2], DT, h.p2);
+        }
+    }
+    if (PARTS & TD_POSITIONS) {
+        h.q0 = sm_mad(h.v0, DT, h.q0); h.q1 = sm_mad(h.v1, DT, h.q1); h.q2 = sm_mad(h.v2, DT, h.q2);
+        h.g0 = sm_mad(h.w0, DT, h.g0); h.g1 = sm_mad(h.w1, DT, h.g1); h.g2 = sm_mad(h.w2, DT, h.g2);
+    }
+}
+
 /* --------------------------------------------------- one physics tick */
 /* Robot.step (src/robot.py:670-678): update_dynamics (:854-858) with
  * _newton_equations (:789-823), _euler_equations (:825-851),
@@ -685,164 +864,7 @@ SD bool tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     double k32[C32_N];
     if (!LATE32 && !STEADY)
         for (int k = 0; k < C32_N; ++k) k32[k] = c32[k];
-    const Geo& g = h.geo;
-    const double m = g.m;
-    /* coefficients of this cycle: the reference's means, or (RAND) the
-     * Robot._randomize_parameters draw of set_control */
-    const double cd = RAND ? h.rnd.cd : CD, dfr = RAND ? h.rnd.dfr : DRAG_FORCE_RATIO,
-                 dtr = RAND ? h.rnd.dtr : DRAG_TORQUE_RATIO;
-    const double cam0 = RAND ? h.rnd.amf0 : AMF0, cam1 = RAND ? h.rnd.amf1 : AMF1,
-                 cam2 = RAND ? h.rnd.amf2 : AMF2;
-    const double car0 = RAND ? h.rnd.amrf0 : AMRF, car1 = RAND ? h.rnd.amrf1 : AMRF,
-                 car2 = RAND ? h.rnd.amrf2 : AMRF;
-    const double cat0 = RAND ? h.rnd.amt0 : AMT0, cat1 = RAND ? h.rnd.amt1 : AMT1,
-                 cat2 = RAND ? h.rnd.amt2 : AMT2;
-    /* OUDisturbance.sample (src/robot.py:233-242) of the force (x, y kept) and
-     * torque (z kept) processes, src/robot.py:796-800, 834-838 */
-    double nf0 = 0.0, nf1 = 0.0, nt2 = 0.0;
-    if (RAND && P.rand_dist) {
-        double z0, z1, z2;
-        sr_normals3(P.seed, h.env_id, (uint64_t)h.rnd.tick, &z0, &z1, &z2);
-        h.rnd.tick += 1.0;
-        h.rnd.ouf0 = sr_ou_step(h.rnd.ouf0, SR_OU_FORCE_THETA, SR_OU_FORCE_SIGMA, z0);
-        h.rnd.ouf1 = sr_ou_step(h.rnd.ouf1, SR_OU_FORCE_THETA, SR_OU_FORCE_SIGMA, z1);
-        h.rnd.out2 = sr_ou_step(h.rnd.out2, SR_OU_TORQUE_THETA, SR_OU_TORQUE_SIGMA, z2);
-        nf0 = h.rnd.ouf0; nf1 = h.rnd.ouf1; nt2 = h.rnd.out2;
-    }
-    /* ---------------- Newton ---------------- */
-    /* Coriolis force -w x (M v)  (src/dynamics.py:159-162) */
-    double mv0 = m * h.v0, mv1 = m * h.v1, mv2 = m * h.v2;
-    double cf0 = -cross_c(h.w1, mv2, h.w2, mv1), cf1 = -cross_c(h.w2, mv0, h.w0, mv2),
-           cf2 = -cross_c(h.w0, mv1, h.w1, mv0);
-    /* drag force (src/dynamics.py:110-116); product mode: (k C v) (|v| + ratio) */
-    const double vnr = np_norm3(h.v0, h.v1, h.v2) + dfr;
-    double df0 = (g.kc0 * h.v0) * vnr;
-    double df1 = (g.kc1 * h.v1) * vnr;
-    double df2 = (g.kc1 * h.v2) * vnr;
-    /* jet force, JET phase only (src/robot.py:937-951, src/dynamics.py:87-101) */
-    const bool jet = !SETTLED && h.phase == JET;
-    double jf0 = jet ? g.mr * (h.d0 * g.speed) * -cd : 0.0;
-    double jf1 = jet ? g.mr * (h.d1 * g.speed) * -cd : 0.0;
-    double jf2 = jet ? g.mr * (h.d2 * g.speed) * -cd : 0.0;
-    /* added-mass force (src/dynamics.py:131-141) */
-    const double mr = SETTLED ? 0.0 : g.mr;
-    double am0 = m * cam0, am1 = m * cam1, am2 = m * cam2;
-    double amr0 = mr * car0, amr1 = mr * car1, amr2 = mr * car2;
-    double amv0 = am0 * h.v0, amv1 = am1 * h.v1, amv2 = am2 * h.v2;
-    double af0 = -sm_mad(amr0, h.v0, sm_mad(am0, h.a0, cross_c(h.w1, amv2, h.w2, amv1)));
-    double af1 = -sm_mad(amr1, h.v1, sm_mad(am1, h.a1, cross_c(h.w2, amv0, h.w0, amv2)));
-    double af2 = -sm_mad(amr2, h.v2, sm_mad(am2, h.a2, cross_c(h.w0, amv1, h.w1, amv0)));
-    /* fictitious forces of the moving center of mass (src/robot.py:806-810);
-     * com = (cx, 0, 0) */
-    const double cx = h.com, crx = SETTLED ? 0.0 : h.comr;
-    double acc_y = (h.w0 * (h.w1 * cx) + (h.w2 * crx) * 2.0) + h.al2 * cx;
-    double acc_z = (h.w0 * (h.w2 * cx) + -(h.w1 * crx) * 2.0) + -(h.al1 * cx);
-    double acc_x = cross_c(h.w1, -(h.w1 * cx), h.w2, h.w2 * cx) + (SETTLED ? 0.0 : h.coma);
-    /* total force and linear acceleration (src/dynamics.py:5-10) */
-    /* F * (1/m) (product mode; src/dynamics.py:5-10 solves diag(m) a = F) */
-    double na0, na1, na2;
-    const double rm = g.rm;
-    if (RAND) {   /* + force noise (z: zero) */
-        na0 = sm_mad(acc_x, m, (((jf0 + df0) + af0) + cf0) + nf0) * rm;
-        na1 = sm_mad(acc_y, m, (((jf1 + df1) + af1) + cf1) + nf1) * rm;
-        na2 = sm_mad(acc_z, m, (((jf2 + df2) + af2) + cf2) + 0.0) * rm;
-    } else {
-        na0 = sm_mad(acc_x, m, ((jf0 + df0) + af0) + cf0) * rm;
-        na1 = sm_mad(acc_y, m, ((jf1 + df1) + af1) + cf1) * rm;
-        na2 = sm_mad(acc_z, m, ((jf2 + df2) + af2) + cf2) * rm;
-    }
-    /* ---------------- Euler ---------------- */
-    const double I0 = g.I0, I1 = g.I1;
-    /* Coriolis torque -w x (I w) (src/dynamics.py:165-168) */
-    double iw0 = I0 * h.w0, iw1 = I1 * h.w1, iw2 = I1 * h.w2;
-    double ct0 = -cross_c(h.w1, iw2, h.w2, iw1), ct1 = -cross_c(h.w2, iw0, h.w0, iw2),
-           ct2 = -cross_c(h.w0, iw1, h.w1, iw0);
-    /* drag torque (src/dynamics.py:119-128); product mode: (C k A w) (|w| dims + width ratio) */
-    const double wn = np_norm3(h.w0, h.w1, h.w2), wr = h.W * dtr;
-    const double sx = sm_fma(wn, g.dimx, wr), sy = sm_fma(wn, g.dimy, wr);
-    double dt0 = (g.ra0 * h.w0) * sx;
-    double dt1 = (g.ra1 * h.w1) * sy;
-    double dt2 = (g.ra1 * h.w2) * sy;
-    /* jet torque r x F, r = (mid_x - L/2, 0, 0) (src/robot.py:931-935) */
-    double jt1 = -(g.rx * jf2), jt2 = g.rx * jf1;
-    /* deformation torque -(dI/dt) w; prev_I <- I (src/robot.py:888-896) */
-    double ir0 = 0.0, ir1 = 0.0, ir2 = 0.0;   /* settled: (I - prev_I) / dt = +0 / dt */
-    if (!SETTLED) {
-        ir0 = div_dt(I0 - h.pI0);
-        ir1 = div_dt(I1 - h.pI1);
-        ir2 = ir1;
-        if (h.pI2 != h.pI1) ir2 = div_dt(I1 - h.pI2);   /* prev_I[1,1] == prev_I[2,2] always */
-        h.pI0 = I0; h.pI1 = I1; h.pI2 = I1;
-    }
-    double dft0 = -(ir0 * h.w0), dft1 = -(ir1 * h.w1), dft2 = -(ir2 * h.w2);
-    /* added-mass torque, I_rate term identically zero (src/dynamics.py:144-156) */
-    double at0 = I0 * cat0, at1 = I1 * cat1, at2 = I1 * cat2;
-    double atw0 = at0 * h.w0, atw1 = at1 * h.w1, atw2 = at2 * h.w2;
-    double amt0 = -(sm_mad(at0, h.al0, cross_c(h.w1, atw2, h.w2, atw1)) + cross_c(h.v1, amv2, h.v2, amv1));
-    double amt1 = -(sm_mad(at1, h.al1, cross_c(h.w2, atw0, h.w0, atw2)) + cross_c(h.v2, amv0, h.v0, amv2));
-    double amt2 = -(sm_mad(at2, h.al2, cross_c(h.w0, atw1, h.w1, atw0)) + cross_c(h.v0, amv1, h.v1, amv0));
-    /* total torque and angular acceleration (src/dynamics.py:13-17) */
-    /* tau * (1/I) (product mode; src/dynamics.py:13-17) */
-    double nal0, nal1, nal2;
-    const double rI0 = g.rI0, rI1 = g.rI1;
-    if (RAND) {   /* + torque noise (x, y: zero) */
-        nal0 = ((sm_mad(-ir0, h.w0, dt0 + ct0) + amt0) + 0.0) * rI0;
-        nal1 = ((sm_mad(-ir1, h.w1, (jt1 + dt1) + ct1) + amt1) + 0.0) * rI1;
-        nal2 = ((sm_mad(-ir2, h.w2, (jt2 + dt2) + ct2) + amt2) + nt2) * rI1;
-    } else {
-        nal0 = (sm_mad(-ir0, h.w0, dt0 + ct0) + amt0) * rI0;
-        nal1 = (sm_mad(-ir1, h.w1, (jt1 + dt1) + ct1) + amt1) * rI1;
-        nal2 = (sm_mad(-ir2, h.w2, (jt2 + dt2) + ct2) + amt2) * rI1;
-    }
-    if (REC) {
-        const double z = 0.0;
-        auto put = [&](int col, double x) { rec[(int64_t)col * rs] = x; };
-        put(SALP_T_JETV0, jet ? h.d0 * g.speed : 0.0);
-        put(SALP_T_JETV1, jet ? h.d1 * g.speed : 0.0);
-        put(SALP_T_JETV2, jet ? h.d2 * g.speed : 0.0);
-        put(SALP_T_JETF0, jf0); put(SALP_T_JETF1, jf1); put(SALP_T_JETF2, jf2);
-        put(SALP_T_JETT0, z * jf2 - z * jf1); put(SALP_T_JETT1, jt1); put(SALP_T_JETT2, jt2);
-        put(SALP_T_DRAGF0, df0); put(SALP_T_DRAGF1, df1); put(SALP_T_DRAGF2, df2);
-        put(SALP_T_DRAGT0, dt0); put(SALP_T_DRAGT1, dt1); put(SALP_T_DRAGT2, dt2);
-        put(SALP_T_CORF0, cf0); put(SALP_T_CORF1, cf1); put(SALP_T_CORF2, cf2);
-        put(SALP_T_CORT0, ct0); put(SALP_T_CORT1, ct1); put(SALP_T_CORT2, ct2);
-        put(SALP_T_AMF0, af0); put(SALP_T_AMF1, af1); put(SALP_T_AMF2, af2);
-        put(SALP_T_AMT0, amt0); put(SALP_T_AMT1, amt1); put(SALP_T_AMT2, amt2);
-        put(SALP_T_DEFT0, dft0); put(SALP_T_DEFT1, dft1); put(SALP_T_DEFT2, dft2);
-        put(SALP_T_ACCF0, acc_x * m); put(SALP_T_ACCF1, acc_y * m); put(SALP_T_ACCF2, acc_z * m);
-    }
-    h.a0 = na0; h.a1 = na1; h.a2 = na2;
-    h.al0 = nal0; h.al1 = nal1; h.al2 = nal2;
-    /* ---------------- integrate (semi-implicit Euler) ---------------- */
-    h.v0 = sm_mad(na0, DT, h.v0); h.v1 = sm_mad(na1, DT, h.v1); h.v2 = sm_mad(na2, DT, h.v2);
-    h.w0 = sm_mad(nal0, DT, h.w0); h.w1 = sm_mad(nal1, DT, h.w1); h.w2 = sm_mad(nal2, DT, h.w2);
-    {   /* to_euler_angle_rate_jit (src/dynamics.py:20-31) at the current angles;
-         * product mode (the oracle's to_euler_angle_rate): u = sin(phi) w1 +
-         * cos(phi) w2, g = u / cos(theta) is row 2 and tan(theta) u = sin(theta) g
-         * row 0's tail */
-        const double u = sm_fma(h.cp, h.w2, h.sp * h.w1);
-        const double g2 = qdiv(u, rcp_of(h.cth));
-        double r0 = sm_fma(h.st, g2, h.w0);
-        double r1 = sm_fma(-h.sp, h.w2, h.cp * h.w1);
-        double r2 = g2;
-        h.e0 = sm_mad(r0, DT, h.e0); h.e1 = sm_mad(r1, DT, h.e1); h.e2 = sm_mad(r2, DT, h.e2);
-        if (REC) {
-            rec[(int64_t)SALP_T_ETAR0 * rs] = r0;
-            rec[(int64_t)SALP_T_ETAR1 * rs] = r1;
-            rec[(int64_t)SALP_T_ETAR2 * rs] = r2;
-        }
-    }
-    {   /* to_world_frame_jit (src/dynamics.py:34-58) at the new angles (world_frame;
-         * roll / pitch sin / cos kept for the next tick's Euler-rate map) */
-        double ss, cs;
-        sm_sincos_rp2(h.e0, h.e1, &h.sp, &h.cp, &h.st, &h.cth, P.sk);
-        sm_sincos_yaw_p(h.e2, &ss, &cs, P.sk);
-        double vw[3];
-        sm_world_frame(h.sp, h.cp, h.st, h.cth, ss, cs, h.v0, h.v1, h.v2, vw);
-        h.p0 = sm_mad(vw[0], DT, h.p0); h.p1 = sm_mad(vw[1], DT, h.p1); h.p2 = sm_mad(vw[2], DT, h.p2);
-    }
-    h.q0 = sm_mad(h.v0, DT, h.q0); h.q1 = sm_mad(h.v1, DT, h.q1); h.q2 = sm_mad(h.v2, DT, h.q2);
-    h.g0 = sm_mad(h.w0, DT, h.g0); h.g1 = sm_mad(h.w1, DT, h.g1); h.g2 = sm_mad(h.w2, DT, h.g2);
+    tick_dynamics<REC, RAND, SETTLED>(h, P, rec, rs);
     /* ---------------- clocks, phase, properties ---------------- */
     h.ct += DT;
     h.time += DT;

@@ -60,6 +60,88 @@ __device__ __forceinline__ void run_cycle(Hot& h, const Params& P, salp::Cache32
     for (; h.ct < h.b2 && g < kMaxTicksPerCycle; ++g) salp::tick<false, RAND, false, true, true>(h, PV, c32);
 }
 
+// ---------------------------------------------------------------- one env per workgroup
+// The per-env step path (SalpRobotEnv.step: one env, one launch per env-step)
+// is a latency: one lane runs the ~700 ticks of a cycle back to back while the
+// rest of the chip idles.  k_step_wave gives every env a workgroup of two waves
+// and splits each tick along two one-way dependences of Robot.step:
+// * the geometry (update_properties: body length / width, volume, centre of
+//   mass, mass, inertia, drag coefficients, jet rates; src/robot.py:640-668,
+//   1055-1066) depends on the cycle's constants and the clock only, never on
+//   the motion: wave 0's 64 lanes compute the geometry after each of the next
+//   64 ticks at once (lane j: tick j; the values that chain from one tick to
+//   the next - previous volume, float32 flag, centre of mass and its rate -
+//   come from lane j - 1 by a shuffle) into an LDS table;
+// * the forces and the velocity integration (tick_dynamics' TD_FORCES) never read the Euler
+//   angles or the world position: wave 0 runs them on the table's geometry and
+//   hands each tick's new velocities to wave 1 through an LDS ring; wave 1 runs
+//   the angle / world-frame chain (TD_KINEMATICS) behind it.
+// Every value is the expression tick() computes, evaluated on the same operands:
+// results are those of k_step bit for bit (tests/test_gpu_step_wave.py).  A tick
+// then costs wave 0 its forces plus a 1/64 share of the geometry.
+enum {
+    WG_CT, WG_TIME, WG_PHASE, WG_W, WG_COM, WG_COMR, WG_COMA,
+    WG_M, WG_MR, WG_I0, WG_I1, WG_KC0, WG_KC1, WG_RA0, WG_RA1, WG_DIMX, WG_DIMY, WG_SPEED, WG_RX,
+    WG_RM, WG_RI0, WG_RI1,                       /* read by every tick (22) */
+    WG_L, WG_V, WG_PV, WG_G32, WG_PV32,          /* read after the block's last tick */
+    WG_STRIDE = 28                               /* doubles per row (16-B aligned rows) */
+};
+constexpr int kWave = 64;
+
+// Row j of the table: the geometry state after tick j of the block that starts
+// at the lane's (uniform) state h; tick()'s clocks / update_state /
+// update_properties / rates, in the same order on the same operands.
+__device__ __forceinline__ void wave_geometry_rows(const Hot& h, const Params& P, salp::Cache32 c32, double* rows) {
+    using namespace salp;
+    const int j = (int)(threadIdx.x & (kWave - 1));
+    double ct = h.ct, tm = h.time, my_ct = 0.0, my_tm = 0.0;
+    for (int k = 0; k < kWave; ++k) {   /* cycle_time / time after k + 1 ticks: the same sums */
+        ct += DT;
+        tm += DT;
+        my_ct = k == j ? ct : my_ct;
+        my_tm = k == j ? tm : my_tm;
+    }
+    int ph = my_ct <= h.b2 ? COAST : REST;
+    ph = my_ct <= h.b1 ? JET : ph;
+    ph = my_ct <= h.mx ? REFILL : ph;
+    double L, W;
+    bool f;
+    body_lw(P, ph, my_ct, h.refill, h.mx, h.c, h.cr, h.rr, h.c32, &L, &W, &f);
+    const Core c = core(L, W, false);
+    double V = water_volume(P, c, false);
+    double wm = water_mass(P, V, false);
+    double com = center_of_mass(P, c, wm, false);
+    Geo ng = make_geo_shape(P, c, L, W, wm, false);
+    if (f) {
+        V = c32[C32_V]; wm = c32[C32_WM]; com = c32[C32_COM];
+        ng.m = c32[C32_M]; ng.I0 = c32[C32_I0]; ng.I1 = c32[C32_I1];
+        ng.kc0 = c32[C32_KC0]; ng.kc1 = c32[C32_KC1]; ng.ra0 = c32[C32_RA0]; ng.ra1 = c32[C32_RA1];
+        ng.dimx = c32[C32_DIMX]; ng.dimy = c32[C32_DIMY];
+    }
+    /* the previous tick's volume, float32 flag and centre of mass: lane j - 1 (lane 0: the block's start) */
+    double pV = __shfl_up(V, 1), pcom = __shfl_up(com, 1);
+    int pv32 = __shfl_up((int)f, 1);
+    if (j == 0) {
+        pV = h.V;
+        pcom = h.com;
+        pv32 = h.g32;
+    }
+    const double comr = div_dt(com - pcom);
+    double pcomr = __shfl_up(comr, 1);
+    if (j == 0) pcomr = h.comr;
+    const double coma = div_dt(comr - pcomr);
+    jet_rates(P, V, pV, wm, f, pv32 != 0, ng);
+    geo_recips(ng);
+    double* r = rows + j * WG_STRIDE;
+    r[WG_CT] = my_ct; r[WG_TIME] = my_tm; r[WG_PHASE] = (double)ph; r[WG_W] = W;
+    r[WG_COM] = com; r[WG_COMR] = comr; r[WG_COMA] = coma;
+    r[WG_M] = ng.m; r[WG_MR] = ng.mr; r[WG_I0] = ng.I0; r[WG_I1] = ng.I1;
+    r[WG_KC0] = ng.kc0; r[WG_KC1] = ng.kc1; r[WG_RA0] = ng.ra0; r[WG_RA1] = ng.ra1;
+    r[WG_DIMX] = ng.dimx; r[WG_DIMY] = ng.dimy; r[WG_SPEED] = ng.speed; r[WG_RX] = ng.rx;
+    r[WG_RM] = ng.rm; r[WG_RI0] = ng.rI0; r[WG_RI1] = ng.rI1;
+    r[WG_L] = L; r[WG_V] = V; r[WG_PV] = pV; r[WG_G32] = f ? 1.0 : 0.0; r[WG_PV32] = pv32 ? 1.0 : 0.0;
+}
+
 // The loop of Robot.step_through_cycle with record=True (src/robot.py:
 // 750-765): sample 0 before the first tick, one sample per tick after it.
 template <bool RAND>
@@ -997,6 +1079,149 @@ __device__ __forceinline__ void pair_publish(int* flag, int value) {
     __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// k_step_wave's LDS: the geometry table (wave 0), the velocity ring (wave 0 ->
+// wave 1) with its two counters, and wave 1's hand-over of the angle chain.
+constexpr int kWaveRing = 64;                       // ticks wave 0 may run ahead
+enum { WR_V0, WR_V1, WR_V2, WR_W0, WR_W1, WR_W2, WR_STRIDE = 6 };
+enum { WX_E0, WX_E1, WX_E2, WX_P0, WX_P1, WX_P2, WX_SP, WX_CP, WX_ST, WX_CTH, WX_N };
+struct WaveShared {
+    double rows[kWave * WG_STRIDE];
+    double ring[kWaveRing * WR_STRIDE];
+    double xchg[WX_N];
+    double c32[salp::C32_N];
+    int produced, consumed;   // ticks of this cycle wave 0 has published / wave 1 has read
+};
+
+// One breathing cycle of the env both waves hold (Robot.step_through_cycle's
+// loop, src/robot.py:750-765).  Both waves run the same clock (the same sums),
+// so they agree on the cycle's tick count.  Returns false if a wait gave up
+// (g_pair_timeouts counts it; the env's results are then invalid).
+template <bool RAND>
+__device__ __forceinline__ bool run_cycle_split(Hot& h, const Params& P, salp::Cache32 c32, WaveShared& W) {
+    const bool kin = threadIdx.x >= kWave;
+    bool ok = true;
+    int g = 0;
+    if (!kin) {
+        while (h.ct < h.b2 && g < kMaxTicksPerCycle) {
+            wave_geometry_rows(h, P, c32, W.rows);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   /* rows of the other lanes */
+            int last = 0;
+            for (int j = 0; j < kWave && h.ct < h.b2 && g < kMaxTicksPerCycle; ++j, ++g) {
+                /* the row is read before the forces, so that its LDS latency hides under them */
+                double x[WG_RI1 + 1];
+                const double* r = W.rows + j * WG_STRIDE;
+#pragma unroll
+                for (int k = 0; k <= WG_RI1; ++k) x[k] = r[k];
+                /* the forces' SETTLED instance where its constants are the values the lane holds
+                 * (jet force off, water-mass rate, centre-of-mass rate and acceleration
+                 * +0, inertia unchanged): the same results with less arithmetic (tick) */
+                const bool settled = h.phase != salp::JET &&
+                                     (__double_as_longlong(h.geo.mr) | __double_as_longlong(h.comr) |
+                                      __double_as_longlong(h.coma)) == 0 &&
+                                     h.geo.I0 == h.pI0 && h.geo.I1 == h.pI1 && h.pI2 == h.pI1;
+                if (settled)
+                    salp::tick_dynamics<false, RAND, true, salp::TD_FORCES | salp::TD_POSITIONS>(h, P, nullptr, 0);
+                else
+                    salp::tick_dynamics<false, RAND, false, salp::TD_FORCES | salp::TD_POSITIONS>(h, P, nullptr, 0);
+                /* this tick's velocities to wave 1 (a slot it has read) */
+                if (g >= kWaveRing) ok = pair_wait(&W.consumed, g - kWaveRing + 1) && ok;
+                double* q = W.ring + (g % kWaveRing) * WR_STRIDE;
+                q[WR_V0] = h.v0; q[WR_V1] = h.v1; q[WR_V2] = h.v2;
+                q[WR_W0] = h.w0; q[WR_W1] = h.w1; q[WR_W2] = h.w2;
+                pair_publish(&W.produced, g + 1);
+                h.ct = x[WG_CT]; h.time = x[WG_TIME]; h.phase = (int)x[WG_PHASE]; h.W = x[WG_W];
+                h.com = x[WG_COM]; h.comr = x[WG_COMR]; h.coma = x[WG_COMA];
+                salp::Geo& q2 = h.geo;
+                q2.m = x[WG_M]; q2.mr = x[WG_MR]; q2.I0 = x[WG_I0]; q2.I1 = x[WG_I1];
+                q2.kc0 = x[WG_KC0]; q2.kc1 = x[WG_KC1]; q2.ra0 = x[WG_RA0]; q2.ra1 = x[WG_RA1];
+                q2.dimx = x[WG_DIMX]; q2.dimy = x[WG_DIMY]; q2.speed = x[WG_SPEED]; q2.rx = x[WG_RX];
+                q2.rm = x[WG_RM]; q2.rI0 = x[WG_RI0]; q2.rI1 = x[WG_RI1];
+                last = j;
+            }
+            const double* r = W.rows + last * WG_STRIDE;
+            h.L = r[WG_L]; h.V = r[WG_V]; h.pV = r[WG_PV];
+            h.g32 = r[WG_G32] != 0.0; h.pv32 = r[WG_PV32] != 0.0;
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   /* the table is rewritten next */
+        }
+    } else {
+        double ct = h.ct;
+        for (; ct < h.b2 && g < kMaxTicksPerCycle; ++g) {
+            ok = pair_wait(&W.produced, g + 1) && ok;
+            const double* q = W.ring + (g % kWaveRing) * WR_STRIDE;
+            h.v0 = q[WR_V0]; h.v1 = q[WR_V1]; h.v2 = q[WR_V2];
+            h.w0 = q[WR_W0]; h.w1 = q[WR_W1]; h.w2 = q[WR_W2];
+            pair_publish(&W.consumed, g + 1);
+            salp::tick_dynamics<false, RAND, false, salp::TD_KINEMATICS>(h, P, nullptr, 0);
+            ct += salp::DT;
+        }
+    }
+    return ok;
+}
+
+// SalpRobotEnv.step with one env per workgroup of two waves (run_cycle_split):
+// env = blockIdx.x; both waves load the env and run begin_step identically
+// (wave 0 stores), run the cycle split, and wave 1 hands the angle chain to
+// wave 0, which ends the env-step (k_step's epilogue) and stores.
+template <bool RAND>
+__global__ __launch_bounds__(2 * kWave) void k_step_wave(double* S, Params P, const float* actions,
+                                                         float* obs_out, double* reward_out,
+                                                         uint8_t* term_out, uint8_t* trunc_out,
+                                                         int auto_reset, float* term_obs_out, double* info_out) {
+    const int64_t i = blockIdx.x;
+    if (i >= P.n) return;
+    __shared__ __attribute__((aligned(16))) WaveShared W;
+    const salp::Cache32 c32{W.c32, 1};
+    const bool kin = threadIdx.x >= kWave;
+    if (threadIdx.x == 0) {
+        W.produced = 0;
+        W.consumed = 0;
+    }
+    Hot h;
+    salp::load_hot<RAND>(h, S, P, i);
+    {
+        salp::ColdRegs<RAND> C;
+        salp::load_cold<RAND>(C, S, P, i);
+        salp::begin_step<RAND>(h, &C, P, i, actions[3 * i], actions[3 * i + 1], actions[3 * i + 2], c32);
+        if (!kin) salp::store_cold<RAND>(C, S, P, i);
+    }
+    __syncthreads();
+    run_cycle_split<RAND>(h, P, c32, W);
+    __syncthreads();
+    if (kin) {
+        if (threadIdx.x == kWave) {
+            double* x = W.xchg;
+            x[WX_E0] = h.e0; x[WX_E1] = h.e1; x[WX_E2] = h.e2;
+            x[WX_P0] = h.p0; x[WX_P1] = h.p1; x[WX_P2] = h.p2;
+            x[WX_SP] = h.sp; x[WX_CP] = h.cp; x[WX_ST] = h.st; x[WX_CTH] = h.cth;
+        }
+    }
+    __syncthreads();
+    if (kin) return;
+    {
+        const double* x = W.xchg;
+        h.e0 = x[WX_E0]; h.e1 = x[WX_E1]; h.e2 = x[WX_E2];
+        h.p0 = x[WX_P0]; h.p1 = x[WX_P1]; h.p2 = x[WX_P2];
+        h.sp = x[WX_SP]; h.cp = x[WX_CP]; h.st = x[WX_ST]; h.cth = x[WX_CTH];
+    }
+    float o[SALP_OBS_DIM_MAX];
+    double* info = info_out ? info_out + (size_t)SALP_INFO_DIM * i : nullptr;
+    salp::ColdRegs<RAND> C;
+    salp::load_cold<RAND>(C, S, P, i);
+    double& sc = salp::sref(&C, P, i, SALP_F_STEP_COUNT);
+    sc = sc + 1.0;
+    const salp::StepOut r = salp::finish_step<RAND>(h, &C, P, i, o, info);
+    if (term_obs_out)
+        for (int k = 0; k < P.obs_dim; ++k) term_obs_out[(size_t)i * P.obs_dim + k] = o[k];
+    if (auto_reset && (r.terminated || r.truncated)) salp::reset_env_philox(h, &C, P, i, o);
+    salp::store_cold<RAND>(C, S, P, i);
+    if (reward_out) reward_out[i] = r.reward;
+    if (term_out) term_out[i] = r.terminated;
+    if (trunc_out) trunc_out[i] = r.truncated;
+    if (obs_out)
+        for (int k = 0; k < P.obs_dim; ++k) obs_out[(size_t)i * P.obs_dim + k] = o[k];
+    salp::store_hot<RAND>(h, S, P, i);
+}
+
 struct ValuesToPartner {
     static constexpr bool kDefer = true;
     PairJobs* J;
@@ -1556,6 +1781,7 @@ struct SalpEnv {
     size_t sort_temp_bytes = 0;
     int64_t* step_counts = nullptr;   // per-env env-step counter of a chained salp_step_random
     int rollout_kernel = -1;          // salp_set_rollout_kernel: -1 auto, 0 k_rollout, 1 k_rollout_pair
+    int step_kernel = -1;             // salp_set_step_kernel: -1 auto, 0 k_step, 1 k_step_wave
     int cu_count = 256;               // compute units of the device (the auto choice)
 };
 
@@ -1626,6 +1852,18 @@ bool use_pair(const SalpEnv* h) {
     return h->n <= (int64_t)h->cu_count * 128;
 }
 unsigned pair_blocks_for(int64_t n) { return (unsigned)((n + kPairEnvs - 1) / kPairEnvs); }
+
+// salp_step's kernel: one wave per env (k_step_wave) for small batches - the
+// per-env SalpRobotEnv and small vector envs, where a lane per env leaves the
+// chip idle and the step is the latency of one cycle - and while not
+// recording (the trace is written by k_step<true>); one lane per env above
+// kStepWaveMaxEnvs, where the waves would share SIMDs.
+constexpr int64_t kStepWaveMaxEnvs = 1024;
+bool use_step_wave(const SalpEnv* h) {
+    if (h->trace.max_samples > 0 || h->n > (int64_t)UINT32_MAX) return false;
+    if (h->step_kernel == 0 || h->step_kernel == 1) return h->step_kernel == 1;
+    return h->n <= kStepWaveMaxEnvs;
+}
 
 // One chained launch on the kernel use_pair chooses.
 int launch_chained(SalpEnv* h, const RolloutArgs& args, bool pol, hipStream_t st, const char* what) {
@@ -1844,6 +2082,12 @@ int salp_step(SalpEnv* h, const float* actions, float* obs_out, double* reward_o
               float* terminal_obs_out, double* info_out, void* stream) {
     if (!h) return fail(nullptr, SALP_EINVAL, "salp_step: null handle");
     if (!actions) return fail(h, SALP_EINVAL, "salp_step: actions is required");
+    if (use_step_wave(h)) {
+        hipLaunchKernelGGL(randomized(h->dp) ? k_step_wave<true> : k_step_wave<false>, dim3((unsigned)h->n),
+                           dim3(2 * kWave), 0, (hipStream_t)stream, h->state, h->dp, actions, obs_out, reward_out,
+                           terminated_out, truncated_out, auto_reset, terminal_obs_out, info_out);
+        return launched(h, "k_step_wave");
+    }
     auto kern = h->trace.max_samples > 0 ? (randomized(h->dp) ? k_step<true, true> : k_step<true, false>)
                                          : (randomized(h->dp) ? k_step<false, true> : k_step<false, false>);
     int rc;
@@ -2029,6 +2273,13 @@ int salp_pair_timeouts(SalpEnv* h, uint64_t* count_out, void* stream) {
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     *count_out = c;
     return check_hip(h, e, "salp_pair_timeouts");
+}
+
+int salp_set_step_kernel(SalpEnv* h, int mode) {
+    if (!h) return fail(nullptr, SALP_EINVAL, "salp_set_step_kernel: null handle");
+    if (mode < -1 || mode > 1) return fail(h, SALP_EINVAL, "salp_set_step_kernel: mode must be -1, 0 or 1");
+    h->step_kernel = mode;
+    return SALP_OK;
 }
 
 int salp_set_rollout_kernel(SalpEnv* h, int mode) {

@@ -20,12 +20,14 @@ draws (grasp_lab_salp_amd/csrc/salp_random.h).  Not on the device (fail
 loudly): pygame rendering / GIF recording / the interactive loop
 (visualisation, src/salp_robot_env.py:586-1595).
 """
+import ctypes
 from typing import Dict, Optional, Tuple
 
 import numpy as np
 import torch
 
-from ._abi import EPISODE_METRIC_KEYS, FIELD, INFO, MAX_OBSTACLES, REWARD_COMPONENT_KEYS
+from . import _lib
+from ._abi import EPISODE_METRIC_KEYS, FIELD, INFO, INFO_DIM, MAX_OBSTACLES, REWARD_COMPONENT_KEYS
 from .batched_env import BatchedSalpEnv
 from .robot import Robot
 from .spaces import Box, GymEnv
@@ -101,6 +103,45 @@ def draw_obstacles(width, height, num_obstacles, obstacle_radius, target):
     return placed
 
 
+class _StepIO:
+    """The per-env step's host boundary at its cheapest: the action goes up
+    through a pinned buffer, salp_step (no auto-reset) writes obs / reward /
+    flags / info into one packed device buffer, which comes back in one copy
+    into a pinned buffer with NumPy views made once; the C ABI is called with
+    pointers made once (BatchedSalpEnv.step validates and allocates per call)."""
+
+    def __init__(self, sim):
+        self.sim = sim
+        od, dev = sim.obs_dim, sim.device
+        parts = [("info", INFO_DIM, np.float64), ("reward", 1, np.float64), ("obs", od, np.float32),
+                 ("terminated", 1, np.uint8), ("truncated", 1, np.uint8)]
+        off, lay = 0, {}
+        for name, count, dt in parts:
+            lay[name] = (off, count, dt)
+            off += (count * np.dtype(dt).itemsize + 15) // 16 * 16
+        self.act_host = torch.empty((1, 3), dtype=torch.float32, pin_memory=True)
+        self.act_np = self.act_host.numpy()
+        self.act_dev = torch.empty((1, 3), dtype=torch.float32, device=dev)
+        self.out_dev = torch.empty(off, dtype=torch.uint8, device=dev)
+        self.out_host = torch.empty(off, dtype=torch.uint8, pin_memory=True)
+        raw = self.out_host.numpy()
+        self.views = {k: raw[o:o + c * np.dtype(dt).itemsize].view(dt) for k, (o, c, dt) in lay.items()}
+        base = self.out_dev.data_ptr()
+        p = {k: ctypes.c_void_p(base + o) for k, (o, _c, _dt) in lay.items()}
+        self.args = (ctypes.c_void_p(self.act_dev.data_ptr()), p["obs"], p["reward"], p["terminated"],
+                     p["truncated"], 0, None, p["info"])
+
+    def step(self, a):
+        sim = self.sim
+        self.act_np[0] = a
+        stream = torch.cuda.current_stream(sim.device)
+        self.act_dev.copy_(self.act_host, non_blocking=True)
+        sim._run(_lib.load().salp_step(sim.handle, *self.args, ctypes.c_void_p(stream.cuda_stream)))
+        self.out_host.copy_(self.out_dev, non_blocking=True)
+        stream.synchronize()
+        return self.views
+
+
 class SalpRobotEnv(GymEnv):
     """The reference task env on the device (see module docstring)."""
 
@@ -137,6 +178,7 @@ class SalpRobotEnv(GymEnv):
         params = robot.salp_params(width=int(width), height=int(height), num_obstacles=int(num_obstacles),
                                    obstacle_radius=float(obstacle_radius))
         self._sim = BatchedSalpEnv(1, params=params, device=device)
+        self._io = _StepIO(self._sim)
         robot._bind(self._sim, 0, owner=self)
         self._last_obs = None
         self._last_info = None
@@ -293,14 +335,11 @@ class SalpRobotEnv(GymEnv):
             self._sim.enable_trace(Robot._trace_capacity())
         elif not record and self._sim._trace is not None:
             self._sim.disable_trace()
-        r = self._sim.step(torch.from_numpy(a[None]), auto_reset=False, want_terminal_obs=False)
-        packed = torch.cat([r.obs[0].double(), r.reward, r.terminated.double(), r.truncated.double(),
-                            r.info[0]]).cpu().numpy()
-        od = self._sim.obs_dim
-        obs = packed[:od].astype(np.float32)[:self._obs_len()]
-        reward, done, truncated = float(packed[od]), bool(packed[od + 1]), bool(packed[od + 2])
+        io = self._io.step(a)
+        obs = io["obs"][:self._obs_len()].copy()
+        reward, done, truncated = float(io["reward"][0]), bool(io["terminated"][0]), bool(io["truncated"][0])
         self._last_obs = obs
-        self._last_info = packed[od + 3:]
+        self._last_info = io["info"].copy()
         if record:
             self.robot._load_history()
         info = {"position_history": self.robot.position_world_history,

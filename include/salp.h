@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define SALP_ABI_VERSION 10
+#define SALP_ABI_VERSION 11
 
 #define SALP_MAX_OBSTACLES 4
 #define SALP_OBS_DIM_MAX (6 + 2 * SALP_MAX_OBSTACLES)
@@ -242,6 +242,14 @@ int salp_set_rollout_kernel(SalpEnv* h, int mode);
  * process; 0 is the only good answer (the Python layer raises otherwise).
  * Diagnostic with no reference counterpart. */
 int salp_pair_timeouts(SalpEnv* h, uint64_t* count_out, void* stream);
+/* Kernel of salp_step (ABI 11): -1 auto (default), 0 one env per lane
+ * (k_step, lock-step), 1 one env per wave (k_step_wave: the wave's lanes
+ * compute the geometry of 64 ticks at once, then run their dynamics; a cycle's
+ * latency drops to about its steady ticks').  Auto: one env per wave up to
+ * 1 024 envs (the per-env SalpRobotEnv.step, src/salp_robot_env.py:196-299,
+ * and small vector envs).  Recording (salp_set_trace) always uses k_step.
+ * Results per env are identical in every mode.  No reference counterpart. */
+int salp_set_step_kernel(SalpEnv* h, int mode);
 
 /* GAE / returns over a rollout buffer: stable_baselines3's
  * RolloutBuffer.compute_returns_and_advantage (stable-baselines3 >= 2.0,
