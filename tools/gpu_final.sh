@@ -1,0 +1,22 @@
+#!/bin/bash
+# One validation pass of a kept change set: the GPU suite,
+# the default bench line, its rocprofv3 kernel statistics and the PMC passes of
+# the headline kernel.  TAG names the outputs under gpurun_out/.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-final}
+set -o pipefail
+echo "== pytest $(date +%T)"
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+    > "gpurun_out/${TAG}_pytest_gpu.txt" 2>&1 || { tail -30 "gpurun_out/${TAG}_pytest_gpu.txt"; exit 1; }
+tail -1 "gpurun_out/${TAG}_pytest_gpu.txt"
+echo "== bench $(date +%T)"
+timeout -k 10 600 python bench.py > "gpurun_out/${TAG}_bench.json" 2> "gpurun_out/${TAG}_bench.err" || exit 1
+tail -c 300 "gpurun_out/${TAG}_bench.json"
+echo "== rocprofv3 stats $(date +%T)"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/${TAG}_prof" -o run \
+    -- python3 bench.py > "gpurun_out/${TAG}_prof_bench.json" 2> "gpurun_out/${TAG}_prof.err" || exit 1
+echo "== pmc $(date +%T)"
+TAG=$TAG bash tools/gpu_pmc.sh || exit 1
+echo "== done $(date +%T)"
