@@ -1,7 +1,7 @@
 #!/bin/bash
 # One validation pass of a kept change set: the GPU suite,
-# the default bench line, its rocprofv3 kernel statistics and the PMC passes of
-# the headline kernel.  TAG names the outputs under gpurun_out/.
+# the default bench line, its rocprofv3 kernel statistics, the PMC passes of
+# the headline kernel and the per-env step path's latency.  TAG names the outputs under gpurun_out/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -19,4 +19,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "gpuru
     -- python3 bench.py > "gpurun_out/${TAG}_prof_bench.json" 2> "gpurun_out/${TAG}_prof.err" || exit 1
 echo "== pmc $(date +%T)"
 TAG=$TAG bash tools/gpu_pmc.sh || exit 1
+echo "== per-env step latency $(date +%T)"
+timeout -k 10 300 python tools/step_latency.py > "gpurun_out/${TAG}_step_latency.json" 2>/dev/null || exit 1
+timeout -k 10 300 python tools/host_path_bench.py > "gpurun_out/${TAG}_host_path.json" 2>/dev/null || exit 1
 echo "== done $(date +%T)"
