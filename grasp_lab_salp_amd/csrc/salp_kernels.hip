@@ -385,10 +385,7 @@ __device__ __forceinline__ float policy_tanh(float x) {
     return copysignf(a < 0.625f ? small : large, x);
 }
 
-template <int NOUT>
-__device__ __forceinline__ void policy_mlp(PolicyW w, int w1, int b1, int w2, int b2, int hw,
-                                           int hb, const float* x, float* out) {
-    float h1[kPH];
+__device__ __forceinline__ void policy_layer1(PolicyW w, int w1, int b1, const float* x, float* h1) {
 #pragma unroll
     for (int j = 0; j < kPH; j += 2) {
         PolicyF2 acc = {w[b1 + j], w[b1 + j + 1]};
@@ -401,6 +398,13 @@ __device__ __forceinline__ void policy_mlp(PolicyW w, int w1, int b1, int w2, in
         h1[j] = policy_tanh(acc.x);
         h1[j + 1] = policy_tanh(acc.y);
     }
+}
+
+template <int NOUT>
+__device__ __forceinline__ void policy_mlp(PolicyW w, int w1, int b1, int w2, int b2, int hw,
+                                           int hb, const float* x, float* out) {
+    float h1[kPH];
+    policy_layer1(w, w1, b1, x, h1);
 #pragma unroll
     for (int c = 0; c < NOUT; ++c) out[c] = 0.0f;
 #pragma unroll 1
@@ -419,6 +423,36 @@ __device__ __forceinline__ void policy_mlp(PolicyW w, int w1, int b1, int w2, in
     }
 #pragma unroll
     for (int c = 0; c < NOUT; ++c) out[c] += w[hb + c];
+}
+
+// The actor's second layer and heads read from a copy in LDS (k_rollout_pair
+// stages it once per workgroup): a row's 64 weights arrive as 16 broadcast
+// 16-B LDS reads, in order, instead of scalar loads whose out-of-order return
+// makes every row wait for its whole burst from L2.  The same operations in the
+// same order as policy_mlp: bit-identical.
+constexpr int kPolL2 = kPH * kPH + kPH + 3 * kPH;   // W2 [64][64], B2 [64], action head [3][64]
+static_assert(SALP_POLICY_PI_B2 == SALP_POLICY_PI_W2 + kPH * kPH && SALP_POLICY_ACT_W == SALP_POLICY_PI_B2 + kPH,
+              "the staged actor tensors are contiguous in the packed policy");
+__device__ __forceinline__ void policy_actor_l2(PolicyW w, const float* l2, const float* x, float* out) {
+    float h1[kPH];
+    policy_layer1(w, SALP_POLICY_PI_W1, SALP_POLICY_PI_B1, x, h1);
+    out[0] = out[1] = out[2] = 0.0f;
+#pragma unroll 1
+    for (int j = 0; j < kPH; ++j) {
+        const float* row = l2 + j * kPH;
+        PolicyF2 acc = {l2[kPH * kPH + j], 0.0f};
+#pragma unroll
+        for (int k = 0; k < kPH; k += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(row + k);
+            acc = __builtin_elementwise_fma(PolicyF2{v.x, v.y}, PolicyF2{h1[k], h1[k + 1]}, acc);
+            acc = __builtin_elementwise_fma(PolicyF2{v.z, v.w}, PolicyF2{h1[k + 2], h1[k + 3]}, acc);
+        }
+        const float t = policy_tanh(acc.x + acc.y);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) out[c] = fmaf(l2[kPH * kPH + kPH + c * kPH + j], t, out[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) out[c] += w[SALP_POLICY_ACT_B + c];
 }
 
 __device__ __forceinline__ void policy_input(const float* o, int obs_dim, float* x) {
@@ -452,14 +486,20 @@ __device__ __forceinline__ void policy_noise(uint64_t seed, uint64_t env_id, uin
 // buffer holds it), V(o) and log N(a; mean, std) summed over the dims, in the
 // expression order of torch.distributions.Normal.log_prob.
 // value == nullptr: the value network is evaluated elsewhere (k_rollout_pair's B wave).
+// l2: the actor's second layer staged in LDS (policy_actor_l2), or nullptr.
+template <bool L2 = false>
 __device__ __forceinline__ void policy_act(const SalpPolicyRollout& R, int obs_dim, const float* o, uint64_t env_id,
-                                           uint64_t step, float a[3], float* value, float* logp) {
+                                           uint64_t step, float a[3], float* value, float* logp,
+                                           const float* l2 = nullptr) {
     const PolicyW w = (PolicyW)R.weights;
     float x[kPIN];
     policy_input(o, obs_dim, x);
     float mean[3];
-    policy_mlp<3>(w, SALP_POLICY_PI_W1, SALP_POLICY_PI_B1, SALP_POLICY_PI_W2, SALP_POLICY_PI_B2, SALP_POLICY_ACT_W,
-                  SALP_POLICY_ACT_B, x, mean);
+    if (L2)
+        policy_actor_l2(w, l2, x, mean);
+    else
+        policy_mlp<3>(w, SALP_POLICY_PI_W1, SALP_POLICY_PI_B1, SALP_POLICY_PI_W2, SALP_POLICY_PI_B2,
+                      SALP_POLICY_ACT_W, SALP_POLICY_ACT_B, x, mean);
     if (value) *value = policy_value(w, x);
     float z[3];
     policy_noise(R.noise_seed, env_id, step, z);
@@ -480,6 +520,8 @@ __device__ __forceinline__ void policy_act(const SalpPolicyRollout& R, int obs_d
 // policy mean and starts the next env-step.
 struct ValuesInPlace {
     static constexpr bool kDefer = false;
+    static constexpr bool kL2 = false;
+    __device__ __forceinline__ const float* l2() const { return nullptr; }
     __device__ __forceinline__ void start_rep() {}
     __device__ __forceinline__ void boot(const float*, int, float, int64_t) {}
     __device__ __forceinline__ void value(const float*, int, int64_t) {}
@@ -611,8 +653,8 @@ __device__ __forceinline__ void rollout_boundary(Hot& h, ST S, const Params& P, 
             if (POL) {
                 if (!fin) ep_start = R.episode_start[i];
                 float raw[3], v, lp;
-                policy_act(R, P.obs_dim, o, env_id, (uint64_t)SF(SALP_F_STEP_COUNT), raw, VS::kDefer ? nullptr : &v,
-                           &lp);
+                policy_act<VS::kL2>(R, P.obs_dim, o, env_id, (uint64_t)SF(SALP_F_STEP_COUNT), raw,
+                                    VS::kDefer ? nullptr : &v, &lp, vs.l2());
                 const size_t row = (size_t)steps * (size_t)P.n + (size_t)i;
                 for (int k = 0; k < P.obs_dim; ++k) R.obs[row * P.obs_dim + k] = o[k];
                 R.actions[row * 3 + 0] = raw[0];
@@ -1055,6 +1097,7 @@ struct PairShared {
 // the B wave evaluates while the A wave goes on (ValuesToPartner).  Same
 // expressions, same results.
 struct PairJobs {
+    __attribute__((aligned(16))) float pi_l2[kPolL2];   // the actor's second layer and heads (policy_actor_l2)
     float boot_obs[4][kPIN][kPairEnvs];
     float val_obs[4][kPIN][kPairEnvs];
     float boot_rew[4][kPairEnvs];
@@ -1224,8 +1267,10 @@ __global__ __launch_bounds__(2 * kWave) void k_step_wave(double* S, Params P, co
 
 struct ValuesToPartner {
     static constexpr bool kDefer = true;
+    static constexpr bool kL2 = true;
     PairJobs* J;
     int grp, s, buf;
+    __device__ __forceinline__ const float* l2() const { return J->pi_l2; }
     __device__ __forceinline__ void start_rep() {
         buf = __hip_atomic_load(&J->cnt[grp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & 3;
     }
@@ -1616,6 +1661,11 @@ __global__ __launch_bounds__(kBlock) void k_rollout_pair(RolloutArgs A) {
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = (int)(threadIdx.x & 63);
     PairJobs* const jobs = pair_jobs_lds<POL>();
+    if (POL) {   /* the actor's second layer into LDS, once per workgroup */
+        const float* src = (const float*)A.R.weights + SALP_POLICY_PI_W2;
+        for (int k = (int)threadIdx.x; k < kPolL2; k += kBlock) jobs->pi_l2[k] = src[k];
+        __syncthreads();
+    }
     if (wave & 1) pair_wave_b<POL>(sh, jobs, A, wave >> 1, lane);
     else pair_wave_a<POL>(sh, jobs, A, wave >> 1, lane);
 }
