@@ -202,7 +202,7 @@ class BatchedSalpEnv:
         self._check(_lib.load().salp_set_step_kernel(self._h, int(mode)))
 
     def pair_timeouts(self):
-        """Partner waits of the two-wave kernel that gave up since the last
+        """Partner waits of the two-wave kernels that gave up since the last
         call (salp_pair_timeouts; synchronises the stream).  Nonzero means some
         env's results of those launches are invalid."""
         c = ctypes.c_uint64(0)
@@ -214,7 +214,8 @@ class BatchedSalpEnv:
         on a partner wave (its envs' results are invalid)."""
         n = self.pair_timeouts()
         if n:
-            raise _lib.SalpError(f"k_rollout_pair: {n} partner wait(s) timed out; the affected envs' results are invalid")
+            raise _lib.SalpError(f"two-wave kernels (k_rollout_pair / k_step_wave): {n} partner wait(s) timed out; "
+                                 "the affected envs' results are invalid")
 
     def rollout(self, tick_budget, buffers=None, steps_done=None, max_steps=0, chunk=64):
         """Chained random-action rollout: each env runs ``tick_budget`` physics

@@ -131,8 +131,20 @@ class _StepIO:
         self.args = (ctypes.c_void_p(self.act_dev.data_ptr()), p["obs"], p["reward"], p["terminated"],
                      p["truncated"], 0, None, p["info"])
 
+    # k_step_wave's two waves meet through LDS once per tick; a wait that gives
+    # up (never seen: a workgroup's waves are co-resident) invalidates the env's
+    # results and is counted on the device.  Read every CHECK_EVERY steps and at
+    # close (a read costs a synchronising copy; include/salp.h salp_pair_timeouts).
+    CHECK_EVERY = 1024
+
+    def check(self):
+        self.sim.check_pair()
+
     def step(self, a):
         sim = self.sim
+        self.n_steps = getattr(self, "n_steps", 0) + 1
+        if self.n_steps % self.CHECK_EVERY == 0:
+            self.check()
         self.act_np[0] = a
         stream = torch.cuda.current_stream(sim.device)
         self.act_dev.copy_(self.act_host, non_blocking=True)
@@ -355,4 +367,5 @@ class SalpRobotEnv(GymEnv):
         raise NotImplementedError("rendering (pygame, src/salp_robot_env.py:1198-1258) is out of scope")
 
     def close(self):
+        self._io.check()
         self._sim.close()
