@@ -4,9 +4,10 @@
 # the headline kernel and of config 5's collection kernel (through
 # tools/collect_pmc_probe.py), and the per-env step path's latency.  Then, here:
 #   python tools/pmc_summary.py TAG
-#   python tools/pmc_summary.py TAG --kernel 'k_rollout_pair<true>' --symbol k_rollout_pairILb1EE \
+#   python tools/pmc_summary.py TAGc --kernel 'k_rollout_pair<true>' --symbol k_rollout_pairILb1EE \
 #       --config-json '{"n_envs": 32768, "n_steps": 256}' --suffix pmc_collect_summary \
-#       --workload-json gpurun_out/TAG_collect_probe.json  TAG names the outputs under gpurun_out/.
+#       --workload-json gpurun_out/TAG_collect_probe.json
+# TAG names the outputs under gpurun_out/ (the collection's PMC passes: TAGc).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -26,7 +27,7 @@ echo "== pmc $(date +%T)"
 TAG=$TAG bash tools/gpu_pmc.sh || exit 1
 echo "== pmc collection $(date +%T)"
 timeout -k 10 300 python tools/collect_pmc_probe.py > "gpurun_out/${TAG}_collect_probe.json" 2>/dev/null || exit 1
-TAG=$TAG PROBE=1 bash tools/gpu_pmc_collect.sh || exit 1
+TAG=${TAG}c PROBE=1 bash tools/gpu_pmc_collect.sh || exit 1
 echo "== per-env step latency $(date +%T)"
 timeout -k 10 300 python tools/step_latency.py > "gpurun_out/${TAG}_step_latency.json" 2>/dev/null || exit 1
 timeout -k 10 300 python tools/host_path_bench.py > "gpurun_out/${TAG}_host_path.json" 2>/dev/null || exit 1
