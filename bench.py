@@ -354,6 +354,33 @@ def collect_roofline(n, T, collect_s, parity):
     return res
 
 
+def per_env_gym_rate(dev, steps=200):
+    """SalpRobotEnv.step, one env, on the host clock (NumPy action in, NumPy
+    obs / reward / flags / info out): the per-env drop-in path of
+    INTEGRATION.md section 1."""
+    import numpy as np
+    from grasp_lab_salp_amd.robot import Nozzle, Robot
+    from grasp_lab_salp_amd.salp_robot_env import SalpRobotEnv
+    nozzle = Nozzle(length1=0.05, length2=0.05, length3=0.05, area=0.00016, mass=1.0)
+    robot = Robot(dry_mass=1.0, init_length=0.3, init_width=0.15, max_contraction=0.06, nozzle=nozzle)
+    robot.nozzle.set_angles(angle1=0.0, angle2=0.0)
+    robot.set_environment(density=1000)
+    genv = SalpRobotEnv(render_mode=None, robot=robot, device=dev.index if dev.index is not None else 0)
+    rng = np.random.default_rng(1)
+    acts = np.stack([rng.uniform(0, 1, steps + 3), rng.uniform(0, 1, steps + 3),
+                     rng.uniform(-1, 1, steps + 3)], 1).astype(np.float32)
+    for k in range(3):
+        genv.step(acts[k])
+    t0 = time.perf_counter()
+    for k in range(3, steps + 3):
+        _, _, term, trunc, _ = genv.step(acts[k])
+        if term or trunc:
+            genv.reset()
+    rate = steps / (time.perf_counter() - t0)
+    genv.close()
+    return rate
+
+
 def dry_run(a, world, rank):
     """Launcher plumbing without a GPU: same rank layout, offsets and
     reductions as the real run, over gloo."""
@@ -484,7 +511,7 @@ def main(argv=None):
     #   outputs, one env-step per launch, as SalpRobotEnv.step / a learner;
     # * chained k-step: salp_step_random(32), every env runs its 32 env-steps back
     #   to back on k_rollout (max_steps) and stops (from 32 env-steps per call on).
-    lock = given = chained32 = None
+    lock = given = chained32 = gym_rate = None
     if not a.no_lockstep:
         env.step_random(1)
         torch.cuda.synchronize()
@@ -503,6 +530,8 @@ def main(argv=None):
                 - torch.tensor([0.0, 0.0, 1.0], device=dev) for _ in range(4)]
         given = 4 * n / timed(lambda: [env.step(x, auto_reset=True) for x in acts])
         chained32 = 32 * n / timed(lambda: env.step_random(32))
+        if rank == 0 and world == 1:
+            gym_rate = per_env_gym_rate(dev)
 
     ppo = None
     if not a.no_ppo:
@@ -564,8 +593,8 @@ def main(argv=None):
                       "env-steps per second",
         "budget_full_tick_equivalents_per_sec": budget_ticks / elapsed,
         "budget_note": "tick_budget counts full-tick equivalents: per chunk a wave runs k full ticks, then "
-                       "(chunk - k) x q / 256 steady ticks (q = 480, a steady tick costs ~0.55 of a full one), so "
-                       "a lane's executed ticks per launch exceed tick_budget by up to q / 256 = 1.875x; "
+                       "(chunk - k) x q / 256 steady ticks (q = 560: a settled tick costs ~0.39 of a full one), so "
+                       "a lane's executed ticks per launch exceed tick_budget by up to q / 256 = 2.19x; "
                        "ticks_per_sec above this rate is expected, not a contradiction",
         "kernel_ms_per_launch": kern_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -580,9 +609,12 @@ def main(argv=None):
         "lockstep_env_steps_per_sec": lock_total,
         "step_given_actions_env_steps_per_sec": given_total,
         "step_random32_chained_env_steps_per_sec": chained32_total,
+        "per_env_gym_step_env_steps_per_sec": gym_rate,
         "step_paths_note": "lockstep: salp_step_random(1) x4 (k_step_random); given actions: salp_step x4 "
                            "with obs/reward/flags out (the SalpRobotEnv.step path); chained: salp_step_random(32) "
-                           "on k_rollout with max_steps (each env 32 env-steps back to back)",
+                           "on k_rollout with max_steps (each env 32 env-steps back to back); per-env gym: the unchanged "
+                           "drop-in SalpRobotEnv.step (one env, src/train_robot.py:11-21's robot) on the host clock, "
+                           "200 env-steps of U(action box) actions, rank 0 of a 1-GPU run (k_step_wave)",
         "divergence": {"diverged_envs_at_end": diverged_total, "envs": n * world,
                        "nonfinite_obs_rows_in_buffer": bad_rows_total, "buffer_rows": cap * n * world,
                        "note": "the reference integrator itself diverges for some actions (jet_time < dt); "

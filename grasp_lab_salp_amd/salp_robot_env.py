@@ -330,7 +330,7 @@ class SalpRobotEnv(GymEnv):
         ob = np.zeros((1, MAX_OBSTACLES, 2), np.float32)
         for k, o in enumerate(self.obstacles):
             ob[0, k] = o
-        obs = self._sim.reset_to(self.target_point[None], ob, [len(self.obstacles)])
+        obs = self._sim.reset_to(np.array(self._target_point, dtype=np.float32)[None], ob, [len(self._obstacles)])
         self.prev_action = np.array([0.0, 0.0, 0.0])
         self.action = np.array([0.0, 0.0, 0.0])
         self._last_obs = obs[0, :self._obs_len()].cpu().numpy()
