@@ -49,9 +49,10 @@ def assert_bits_equal(x, y, what="", nan_payloads=False):
     raise AssertionError(f"{what}: (field, values, nan payloads, signed zeros) {rows[:10]}; value envs {envs}")
 
 
-def make_pair(n, seed=3, **kw):
+def make_pair(n, seed=3, step_kernel=-1, **kw):
     p = default_params(**kw)
     env = BatchedSalpEnv(n, params=p, seed=seed)
+    env.set_step_kernel(step_kernel)
     o = orc.Oracle(p, n, seed=seed)
     return env, o
 
@@ -448,16 +449,18 @@ def test_state_round_trip_through_the_hbm_layout(n):
     assert torch.equal(back.view(torch.int64), st.view(torch.int64))
 
 
+@pytest.mark.parametrize("step_kernel", [0, 1])
 @pytest.mark.parametrize("n", [1, 128])
-def test_steady_body_with_negative_phase_times(n):
+def test_steady_body_with_negative_phase_times(n, step_kernel):
     """The lock-step kernels run a cycle's COAST/REST ticks without the
     geometry once every lane of the wave is there (salp_device.h
     next_tick_steady).  Small contractions give negative refill and jet times
     (the reference's polynomial), so mx + jet < mx: the first ticks are still
     REFILL with a contracted body although cycle_time > mx + jet.  Every env
     of the batch gets such an action (the whole wave votes), 4 env-steps,
-    bit for bit against the oracle; then ordinary actions."""
-    env, o = make_pair(n, seed=21)
+    bit for bit against the oracle; then ordinary actions.  Both salp_step
+    kernels (one env per lane, one env per two-wave workgroup)."""
+    env, o = make_pair(n, seed=21, step_kernel=step_kernel)
     o.reset()
     rng = np.random.default_rng(8)
     for k in range(6):
@@ -471,17 +474,18 @@ def test_steady_body_with_negative_phase_times(n):
             assert (o.state[FIELD["jet_time"]] < 0).all()
 
 
+@pytest.mark.parametrize("step_kernel", [0, 1])
 @pytest.mark.parametrize("job", [0, 3, 17, 21, 22])
-def test_fixture_episode_actions_on_one_env_bit_exact(job):
+def test_fixture_episode_actions_on_one_env_bit_exact(job, step_kernel):
     """The actions of a reference episode (tests/golden/episodes.npz) on a
     single env, HIP lock-step kernel vs oracle, bit for bit after every
     env-step.  A one-env wave votes alone on the steady-body switch, so this
     is where a wrong switch shows (job 3, env-step 24: contraction 0.0022,
     jet time -0.07 s, turn time 0.016 s, i.e. one REFILL tick after
-    cycle_time > mx + jet)."""
+    cycle_time > mx + jet).  Both salp_step kernels."""
     d = load_episodes()
     rows = np.where(d["job_index"] == job)[0]
-    env, o = make_pair(1, seed=job)
+    env, o = make_pair(1, seed=job, step_kernel=step_kernel)
     o.reset()
     o.state[:] = _cpu(env.get_state())
     for k, r in enumerate(rows):
