@@ -65,6 +65,14 @@ MEAN_TICKS_PER_ENV_STEP = 710.4
 HOT_FIELDS = slice(FIELD["v0"], FIELD["ang2"] + 1)   # kinematic state: NaN once an env diverged
 
 
+def summary_order(path):
+    """Profile tags r<round><letters> in the order they were made: r3h < r3z <
+    r3aa < r3at (round, then length, then name); the last matching summary wins."""
+    tag = os.path.basename(path).split("_")[0]
+    rnd = int("".join(ch for ch in tag[1:] if ch.isdigit()) or 0)
+    return (rnd, len(tag), tag)
+
+
 def pmc_profile(n, budget, chunk):
     """The committed PMC summary (tools/pmc_summary.py) measured on this exact
     configuration AND on this exact k_rollout machine code, if any: HBM
@@ -77,12 +85,7 @@ def pmc_profile(n, budget, chunk):
     sha = _codeobj.kernel_sha(LIB_PATH, _codeobj.ROLLOUT_KERNEL)
     best = None
     stale = []
-    def order(path):   # tags r<round><letters>: r3h < r3z < r3aa < r3at (round, then length, then name)
-        tag = os.path.basename(path).split("_")[0]
-        rnd = int("".join(ch for ch in tag[1:] if ch.isdigit()) or 0)
-        return (rnd, len(tag), tag)
-
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")), key=order):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")), key=summary_order):
         try:
             s = json.load(open(path))
         except (OSError, ValueError):
@@ -323,7 +326,7 @@ def collect_roofline(n, T, collect_s, parity):
     sha = _codeobj.kernel_sha(LIB_PATH, _codeobj.PAIR_COLLECT_KERNEL)
     res["kernel_sha16"] = sha
     best, stale = None, []
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_collect_summary.json"))):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_collect_summary.json")), key=summary_order):
         try:
             s = json.load(open(path))
         except (OSError, ValueError):

@@ -1882,6 +1882,20 @@ int32_t pair_steady_q8() {
     return q;
 }
 
+// salp_collect's steady budget on the pair kernel: the policy's actions make
+// other cycles than uniform random ones, and the bench's PPO leg (config 5,
+// 32 768 envs, n_steps 256) runs best at q = 340 with 176-tick chunks (16.9 vs
+// 16.4 M env-steps/s at round 4's 400 / 192; chunk 160-224 x q 280-440,
+// profiles/r5_experiments.md r5aa-r5ac).  SALP_PAIR_COLLECT_Q8 overrides it.
+int32_t pair_collect_steady_q8() {
+    static const int32_t q = [] {
+        const char* e = std::getenv("SALP_PAIR_COLLECT_Q8");
+        const long v = e ? std::strtol(e, nullptr, 10) : 0;
+        return (int32_t)(v > 0 && v < (1 << 16) ? v : 340);
+    }();
+    return q;
+}
+
 // Any randomisation switch on: launch the RAND instantiation of the kernels.
 bool randomized(const Params& d) { return d.rand_dyn || d.rand_dist || d.rand_act || d.rand_obs || d.latency; }
 
@@ -1919,7 +1933,7 @@ bool use_step_wave(const SalpEnv* h) {
 int launch_chained(SalpEnv* h, const RolloutArgs& args, bool pol, hipStream_t st, const char* what) {
     if (use_pair(h)) {
         RolloutArgs pa = args;
-        pa.steady_q8 = pair_steady_q8();
+        pa.steady_q8 = pol ? pair_collect_steady_q8() : pair_steady_q8();
         hipLaunchKernelGGL(pol ? k_rollout_pair<true> : k_rollout_pair<false>, dim3(pair_blocks_for(h->n)),
                            dim3(kBlock), 0, st, pa);
     } else if (pol) {
@@ -2232,13 +2246,14 @@ int salp_collect(SalpEnv* h, const SalpPolicyRollout* r, void* stream) {
     // r2_experiments.md r2x).  k_rollout_pair, whose B wave takes the value
     // network off the A wave's boundary: 192 (32 768 envs, chunk 96 / 128 / 160
     // / 192 / 224 / 256 / 384: 20.2 / 21.3 / 21.5 / 21.9 / 21.6 / 21.2 / 20.9;
-    // profiles/r4_experiments.md r4x).  SALP_COLLECT_CHUNK overrides both.
+    // profiles/r4_experiments.md r4x); round 5: 176 with q = 340
+    // (pair_collect_steady_q8).  SALP_COLLECT_CHUNK overrides both.
     static const int32_t forced_chunk = [] {
         const char* e = std::getenv("SALP_COLLECT_CHUNK");
         const long v = e ? std::strtol(e, nullptr, 10) : 0;
         return (int32_t)(v > 0 && v < 4096 ? v : 0);
     }();
-    const int32_t chunk = forced_chunk ? forced_chunk : use_pair(h) ? 192 : 384;
+    const int32_t chunk = forced_chunk ? forced_chunk : use_pair(h) ? 176 : 384;
     const int64_t n_chunks = (r->n_steps * kMaxTicksPerCycle + chunk - 1) / chunk;
     RolloutArgs args{h->state, h->dp, n_chunks, chunk, rollout_steady_q8(), r->n_steps, b, nullptr, 1, 0, *r};
     return launch_chained(h, args, true, st, "k_rollout(collect)");
