@@ -77,7 +77,11 @@ class SalpPpoMinibatch(ctypes.Structure):
         ("vf_coef", ctypes.c_double),
         ("workspace", ctypes.c_void_p),
         ("stats", ctypes.c_void_p),
+        ("adv_part", ctypes.c_void_p),
     ]
+
+
+ADV_PARTIAL_DOUBLES = 512   # include/salp.h SALP_PPO_ADV_PARTIAL_DOUBLES
 
 
 class SalpPpoAdam(ctypes.Structure):
@@ -155,6 +159,7 @@ SIGNATURES = {
     "salp_ppo_mlp_workspace_doubles": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int]),
     "salp_ppo_mlp_grads": (ctypes.c_int, [ctypes.POINTER(SalpPpoMinibatch), _V]),
     "salp_ppo_mlp_apply": (ctypes.c_int, [ctypes.POINTER(SalpPpoAdam), _V]),
+    "salp_ppo_mlp_adv_partials": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64, _V, _V, _V, _V]),
 }
 
 

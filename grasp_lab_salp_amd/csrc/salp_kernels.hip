@@ -2000,6 +2000,8 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t salp_ppo_loss_launch
 extern "C" __attribute__((visibility("hidden"))) int64_t salp_ppo_mlp_params_impl(int obs_dim);
 extern "C" __attribute__((visibility("hidden"))) int64_t salp_ppo_mlp_offset_impl(int obs_dim, int tensor);
 extern "C" __attribute__((visibility("hidden"))) int64_t salp_ppo_mlp_workspace_impl(int64_t batch, int obs_dim);
+extern "C" __attribute__((visibility("hidden"))) hipError_t salp_ppo_mlp_adv_partials_launch(
+    int64_t B, int64_t n_mb, const int64_t* idx, const float* adv, double* out, void* stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t salp_ppo_mlp_grads_launch(const SalpPpoMinibatch* m,
                                                                                        void* stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t salp_ppo_mlp_apply_launch(const SalpPpoAdam* a,
@@ -2455,6 +2457,15 @@ int salp_ppo_mlp_grads(const SalpPpoMinibatch* m, void* stream) {
         if (!m->params[t]) return fail(nullptr, SALP_EINVAL, "salp_ppo_mlp_grads: null parameter tensor");
     if (!(m->clip_range >= 0)) return fail(nullptr, SALP_EINVAL, "salp_ppo_mlp_grads: clip_range must be >= 0");
     return check_hip(nullptr, salp_ppo_mlp_grads_launch(m, stream), "k_mlp");
+}
+
+int salp_ppo_mlp_adv_partials(int64_t batch, int64_t n_minibatches, const int64_t* idx, const float* advantages,
+                              double* out, void* stream) {
+    if (batch <= 0 || n_minibatches <= 0 || n_minibatches > 65535)
+        return fail(nullptr, SALP_EINVAL, "salp_ppo_mlp_adv_partials: batch > 0 and 0 < n_minibatches <= 65535");
+    if (!idx || !advantages || !out) return fail(nullptr, SALP_EINVAL, "salp_ppo_mlp_adv_partials: null buffer");
+    return check_hip(nullptr, salp_ppo_mlp_adv_partials_launch(batch, n_minibatches, idx, advantages, out, stream),
+                     "k_mlp_adv_sums");
 }
 
 int salp_ppo_mlp_apply(const SalpPpoAdam* a, void* stream) {

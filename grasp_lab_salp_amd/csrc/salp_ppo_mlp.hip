@@ -113,9 +113,13 @@ __device__ __forceinline__ void block_sums(double (&v)[K], double* sh, int nthre
     }
 }
 
+// blockIdx.y: minibatch (rows idx[y * B ...]), part + y * 2 * NADV (one launch
+// per epoch, salp_ppo_mlp_adv_partials; gridDim.y = 1 for one minibatch).
 __global__ __launch_bounds__(256) void k_mlp_adv_sums(int64_t B, const int64_t* __restrict__ idx,
                                                       const float* __restrict__ adv, double* __restrict__ part) {
     __shared__ double sh[4];
+    idx += (int64_t)blockIdx.y * B;
+    part += (int64_t)blockIdx.y * 2 * NADV;
     double s = 0.0, q = 0.0;
     for (int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x; b < B; b += (int64_t)gridDim.x * 256) {
         const double x = adv[idx[b]];
@@ -625,16 +629,28 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t salp_ppo_mlp_grads_l
     const SalpPpoMinibatch& m = *mb;
     const int nb = row_blocks(m.batch);
     const Layout L = make_layout(m.obs_dim);
-    double* adv_part = m.workspace;
-    double* stat_part = adv_part + 2 * NADV;
+    double* const ws_adv = m.workspace;
+    double* stat_part = ws_adv + 2 * NADV;
     float* part = reinterpret_cast<float*>(stat_part + (int64_t)nb * NSTAT);
-    hipLaunchKernelGGL(k_mlp_adv_sums, dim3(NADV), dim3(256), 0, s, m.batch, m.idx, m.advantages, adv_part);
+    const double* adv_part = m.adv_part;
+    if (!adv_part) {
+        hipLaunchKernelGGL(k_mlp_adv_sums, dim3(NADV), dim3(256), 0, s, m.batch, m.idx, m.advantages, ws_adv);
+        adv_part = ws_adv;
+    }
     const int64_t tiles = (m.batch + TR - 1) / TR;
     const int64_t rpb = (tiles + nb - 1) / nb * TR;
     RowArgs a{m, L, rpb, part, stat_part, adv_part};
     hipLaunchKernelGGL(k_mlp_fwd_bwd, dim3(nb), dim3(NT), 0, s, a);
     const int64_t P = L.off[SALP_MLP_N_TENSORS];
     hipLaunchKernelGGL(k_mlp_reduce, dim3((unsigned)((P + 63) / 64)), dim3(NT_RED), 0, s, m, L, nb, part, stat_part);
+    return hipGetLastError();
+}
+
+static_assert(2 * NADV == SALP_PPO_ADV_PARTIAL_DOUBLES, "include/salp.h advantage partials per minibatch");
+extern "C" __attribute__((visibility("hidden"))) hipError_t salp_ppo_mlp_adv_partials_launch(
+        int64_t B, int64_t n_mb, const int64_t* idx, const float* adv, double* out, void* stream) {
+    hipLaunchKernelGGL(k_mlp_adv_sums, dim3(NADV, (unsigned)n_mb), dim3(256), 0, (hipStream_t)stream, B, idx, adv,
+                       out);
     return hipGetLastError();
 }
 

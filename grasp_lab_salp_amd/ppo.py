@@ -37,6 +37,7 @@ installed: its semantics are restated, not pinned by a reference test.
 """
 import ctypes
 import math
+import os
 import time
 
 import torch
@@ -482,12 +483,14 @@ class PPO:
         for i, t in enumerate(self._mlp_tensors):
             self._f_adam.params[i] = t.data_ptr()
 
-    def _fused_minibatch(self, idx, acc, part="all"):
+    def _fused_minibatch(self, idx, acc, part="all", adv_part=None):
         """One SB3 PPO minibatch step through salp_ppo_mlp: gradient of the
         loss over rows `idx` (stats added to `acc`), the gradient all-reduce
         when there are several ranks, then clip_grad_norm_ and Adam.  `part`
         "grads" / "apply" runs only the part before / after the all-reduce
-        (the two graphs of a multi-rank learner)."""
+        (the two graphs of a multi-rank learner).  `adv_part`: this minibatch's
+        advantage partials from salp_ppo_mlp_adv_partials (an epoch's in one
+        launch), else the gradient call computes them."""
         L = _lib.load()
         stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
         if part == "apply":
@@ -500,7 +503,8 @@ class PPO:
                                   old_log_prob=b.log_probs.data_ptr(), advantages=b.advantages.data_ptr(),
                                   returns=b.returns.data_ptr(), grads=self._f_grads.data_ptr(),
                                   clip_range=self._clip(), ent_coef=float(self.ent_coef), vf_coef=float(self.vf_coef),
-                                  workspace=self._f_ws.data_ptr(), stats=acc.data_ptr())
+                                  workspace=self._f_ws.data_ptr(), stats=acc.data_ptr(),
+                                  adv_part=adv_part.data_ptr() if adv_part is not None else None)
         for i, t in enumerate(self._mlp_tensors):
             m.params[i] = t.data_ptr()
         _lib.check(L.salp_ppo_mlp_grads(ctypes.byref(m), stream))
@@ -775,8 +779,11 @@ class PPO:
         graph per epoch, unless M exceeds max_graph_minibatches), each time
         after the next C x batch_size indices of the epoch's permutation are
         copied into it; the last M % C minibatches are a second graph, captured
-        once too.  The same kernels in the same order as minibatch by minibatch
-        (no per-minibatch launch from Python)."""
+        once too.  A graph opens with one launch of the advantage partials of
+        all its minibatches (salp_ppo_mlp_adv_partials, the sums each
+        minibatch's gradient call would otherwise launch for itself).  The same
+        results as minibatch by minibatch (no per-minibatch launch from
+        Python)."""
         N = self.n_steps * self.n_envs
         bs = self.batch_size
         m = N // bs
@@ -794,17 +801,30 @@ class PPO:
             if c != m:
                 self._gperm.copy_(self._perm[:c * bs])
             self._g_clip = self._clip()
+            # the chunk's advantage partials in one launch (salp_ppo_mlp_adv_partials), then its minibatches
+            self._g_advp = torch.empty(c * _lib.ADV_PARTIAL_DOUBLES, dtype=torch.float64, device=self.device)
+
+            epoch_adv = os.environ.get("SALP_PPO_EPOCH_ADV", "1") != "0"   # 0: per minibatch (A/B runs)
+
+            def chunk(k_mb):
+                if epoch_adv:
+                    L = _lib.load()
+                    stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+                    _lib.check(L.salp_ppo_mlp_adv_partials(bs, k_mb, self._gperm.data_ptr(),
+                                                           self.buf.advantages.data_ptr(), self._g_advp.data_ptr(),
+                                                           stream))
+                for k in range(k_mb):
+                    self._fused_minibatch(self._gperm[k * bs:(k + 1) * bs], self._g_acc,
+                                          adv_part=self._g_advp[k * _lib.ADV_PARTIAL_DOUBLES:] if epoch_adv else None)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
-                for s in range(0, c * bs, bs):
-                    self._fused_minibatch(self._gperm[s:s + bs], self._g_acc)
+                chunk(c)
             self._epoch_graph = g
             self._rem_graph = None
-            if rem:   # the ragged tail: a graph of its own over the head of the same buffer
+            if rem:   # the ragged tail: a graph of its own over the head of the same buffers
                 gr = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gr, capture_error_mode=_CAPTURE_MODE):
-                    for s in range(0, rem * bs, bs):
-                        self._fused_minibatch(self._gperm[s:s + bs], self._g_acc)
+                    chunk(rem)
                 self._rem_graph = gr
             fresh = True
         for e in range(self.n_epochs):

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define SALP_ABI_VERSION 11
+#define SALP_ABI_VERSION 12
 
 #define SALP_MAX_OBSTACLES 4
 #define SALP_OBS_DIM_MAX (6 + 2 * SALP_MAX_OBSTACLES)
@@ -330,8 +330,20 @@ typedef struct SalpPpoMinibatch {
     double vf_coef;
     double* workspace;     /* salp_ppo_mlp_workspace_doubles(batch, obs_dim) */
     float* stats;          /* [4] accumulated, or NULL */
+    const double* adv_part; /* ABI 12: this minibatch's advantage partials from
+                               salp_ppo_mlp_adv_partials, or NULL (computed here) */
 } SalpPpoMinibatch;
 int salp_ppo_mlp_grads(const SalpPpoMinibatch* m, void* stream);
+/* The advantage normalisation's partial sums (sum, sum of squares in fp64;
+ * SALP_PPO_ADV_PARTIAL_DOUBLES per minibatch) of n_minibatches consecutive
+ * minibatches of `batch` rows each (minibatch k: idx[k * batch ...]), in one
+ * launch, exactly as salp_ppo_mlp_grads computes them for one minibatch; pass
+ * out + k * SALP_PPO_ADV_PARTIAL_DOUBLES as minibatch k's adv_part (ABI 12:
+ * one launch per epoch instead of one per minibatch).  No reference
+ * counterpart (SB3 PPO.train's advantage normalisation). */
+#define SALP_PPO_ADV_PARTIAL_DOUBLES 512
+int salp_ppo_mlp_adv_partials(int64_t batch, int64_t n_minibatches, const int64_t* idx, const float* advantages,
+                              double* out, void* stream);
 /* clip_grad_norm_(max_grad_norm; <= 0: no clipping) of the flat gradient,
  * then torch.optim.Adam (no weight decay / amsgrad) on the tensors; exp_avg
  * and exp_avg_sq are flat like grads, step [1] is Adam's step count (float32,
