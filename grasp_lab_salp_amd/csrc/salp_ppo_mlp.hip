@@ -513,9 +513,19 @@ __global__ __launch_bounds__(NT_RED) void k_mlp_reduce(SalpPpoMinibatch m, Layou
         m.grads[p] = (float)t;
     }
     if (blockIdx.x == 0 && g == 1 && m.stats) {
+        // every lane's partials loaded at once, then summed in the same order
+        double x[NB_MAX / 64][3];
+#pragma unroll
+        for (int j = 0; j < NB_MAX / 64; ++j) {
+            const int b = l + 64 * j;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) x[j][k] = b < nb ? stat_part[(int64_t)b * NSTAT + k] : 0.0;
+        }
         double t[3] = {0.0, 0.0, 0.0};
-        for (int b = l; b < nb; b += 64)
-            for (int k = 0; k < 3; ++k) t[k] += stat_part[(int64_t)b * NSTAT + k];
+#pragma unroll
+        for (int j = 0; j < NB_MAX / 64; ++j)
+            if (l + 64 * j < nb)
+                for (int k = 0; k < 3; ++k) t[k] += x[j][k];
         for (int o = 32; o > 0; o >>= 1)
             for (int k = 0; k < 3; ++k) t[k] += __shfl_xor(t[k], o, 64);
         if (l == 0) {
@@ -541,6 +551,7 @@ static_assert((int64_t)NT_APPLY * AP_MAX >= 2 * (H * DP + H + H * H + H) + NA * 
 __global__ __launch_bounds__(NT_APPLY) void k_mlp_apply(SalpPpoAdam o, Layout L) {
     __shared__ double sh[NT_APPLY / 64];
     __shared__ float s_coef;
+    __shared__ float s_adam[2];   // lr / (1 - beta1^step), sqrt(1 - beta2^step)
     __shared__ float* s_base[SALP_MLP_N_TENSORS];   // params[t] - off[t]: p indexes it directly
     __shared__ int s_off[SALP_MLP_N_TENSORS];
 #pragma unroll
@@ -569,8 +580,20 @@ __global__ __launch_bounds__(NT_APPLY) void k_mlp_apply(SalpPpoAdam o, Layout L)
             v1[k] = o.exp_avg_sq[p];
             w1[k] = *wp[k];
         }
-        q += (double)g[k] * (double)g[k];
     }
+    // Adam's bias corrections from the step count alone: wave 0 computes them
+    // while the parameter loads are in flight and hands them over with the
+    // norm's barriers (two powf in all 16 waves after those barriers: ~2 us)
+    const float b1 = (float)o.beta1, b2 = (float)o.beta2, lr = (float)o.lr, eps = (float)o.eps;
+    if (threadIdx.x < 64) {
+        const float bc1 = 1.0f - powf(b1, step), bc2 = 1.0f - powf(b2, step);
+        if (threadIdx.x == 0) {
+            s_adam[0] = lr / bc1;
+            s_adam[1] = sqrtf(bc2);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < AP_MAX; ++k) q += (double)g[k] * (double)g[k];
     q = block_sum_d(q, sh, NT_APPLY);
     if (threadIdx.x == 0) {
         const float total = (float)sqrt(q);
@@ -584,9 +607,7 @@ __global__ __launch_bounds__(NT_APPLY) void k_mlp_apply(SalpPpoAdam o, Layout L)
     }
     __syncthreads();
     const float coef = s_coef;
-    const float b1 = (float)o.beta1, b2 = (float)o.beta2, lr = (float)o.lr, eps = (float)o.eps;
-    const float bc1 = 1.0f - powf(b1, step), bc2 = 1.0f - powf(b2, step);
-    const float step_size = lr / bc1, bc2_sqrt = sqrtf(bc2);
+    const float step_size = s_adam[0], bc2_sqrt = s_adam[1];
 #pragma unroll
     for (int k = 0; k < AP_MAX; ++k) {
         const int p = threadIdx.x + k * NT_APPLY;

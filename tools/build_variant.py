@@ -25,7 +25,7 @@ def main():
     shutil.copytree(os.path.join(ROOT, "grasp_lab_salp_amd", "csrc"), os.path.join(d, "grasp_lab_salp_amd", "csrc"))
     shutil.copytree(os.path.join(ROOT, "include"), os.path.join(d, "include"))
     files = [os.path.join(d, "grasp_lab_salp_amd", "csrc", f) for f in ("salp_kernels.hip", "salp_device.h", "salp_pair.h", "salp_gae.hip", "salp_math.h",
-                                                                          "salp_ppo.hip")]
+                                                                          "salp_ppo.hip", "salp_ppo_mlp.hip")]
     for r in reps:
         old, new = r.split("=>", 1)
         old, new = old.replace("\\n", "\n"), new.replace("\\n", "\n")
