@@ -65,6 +65,9 @@ MEAN_TICKS_PER_ENV_STEP = 710.4
 HOT_FIELDS = slice(FIELD["v0"], FIELD["ang2"] + 1)   # kinematic state: NaN once an env diverged
 
 
+STEADY_WARM, STEADY_TIMED = 40, 20
+
+
 def summary_order(path):
     """Profile tags r<round><letters> in the order they were made: r3h < r3z <
     r3aa < r3at (round, then length, then name); the last matching summary wins."""
@@ -536,6 +539,28 @@ def main(argv=None):
         if rank == 0 and world == 1:
             gym_rate = per_env_gym_rate(dev)
 
+    # The same workload past its start-up transient: envs created and reset
+    # together start their cycles in step and with roll / pitch near zero; over
+    # the first ~25 launches the phases spread and the population's roll /
+    # pitch spread too (tumbling envs), which costs every wave with such a lane
+    # the full sin / cos path.  A fresh handle of the same
+    # size runs STEADY_WARM untimed launches, then STEADY_TIMED timed ones.
+    steady = None
+    if not a.no_lockstep and world == 1:
+        senv = BatchedSalpEnv(n, params=default_params(), seed=a.seed + 7, device=dev.index)
+        sdone = torch.zeros(n, dtype=torch.int64, device=dev)
+        for _ in range(STEADY_WARM):
+            senv.rollout(a.tick_budget, buffers=bufs, steps_done=sdone, chunk=a.chunk)
+        torch.cuda.synchronize()
+        s_0 = int(sdone.sum())
+        ts0 = time.perf_counter()
+        for _ in range(STEADY_TIMED):
+            senv.rollout(a.tick_budget, buffers=bufs, steps_done=sdone, chunk=a.chunk)
+        torch.cuda.synchronize()
+        steady = (int(sdone.sum()) - s_0) / (time.perf_counter() - ts0)
+        senv.close()
+        del senv
+
     ppo = None
     if not a.no_ppo:
         del bufs
@@ -613,6 +638,10 @@ def main(argv=None):
         "step_given_actions_env_steps_per_sec": given_total,
         "step_random32_chained_env_steps_per_sec": chained32_total,
         "per_env_gym_step_env_steps_per_sec": gym_rate,
+        "steady_state_env_steps_per_sec": steady,
+        "steady_state_note": f"the same workload on a fresh handle after {STEADY_WARM} untimed launches, "
+                             f"{STEADY_TIMED} timed (rank 0 of a 1-GPU run): past the start-up transient that value's "
+                             "launches (after `warmup`) still partly cover (DESIGN.md section 5)",
         "step_paths_note": "lockstep: salp_step_random(1) x4 (k_step_random); given actions: salp_step x4 "
                            "with obs/reward/flags out (the SalpRobotEnv.step path); chained: salp_step_random(32) "
                            "on k_rollout with max_steps (each env 32 env-steps back to back); per-env gym: the unchanged "
