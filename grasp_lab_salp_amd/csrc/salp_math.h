@@ -308,8 +308,10 @@ SM_QUAL void sm_sincos_short_p(double x, double* s_out, double* c_out, SmPoly K)
 /* sin / cos of roll x0 and pitch x1 together: the short kernels for both when
  * neither |x| exceeds 1/16 (NaN included: the kernels return NaN for it, and a
  * diverged env's NaN angles do not send its wave down the long path), else
- * fdlibm's sm_sincos_p for both.  The choice is a function of (x0, x1) alone
+ * the yaw's sm_sincos_yaw_p for both (fdlibm's sm_sincos_p without
+ * SALP_FMA).  The choice is a function of (x0, x1) alone
  * (per lane, not per wave), so results do not depend on the other lanes. */
+SM_QUAL void sm_sincos_yaw_p(double x, double* s_out, double* c_out, SmPoly K);
 SM_QUAL void sm_sincos_rp2(double x0, double x1, double* s0, double* c0, double* s1, double* c1, SmPoly K) {
 #if SALP_FMA
     if (!(fabs(x0) > SM_SHORT_MAX || fabs(x1) > SM_SHORT_MAX)) {
@@ -317,9 +319,15 @@ SM_QUAL void sm_sincos_rp2(double x0, double x1, double* s0, double* c0, double*
         sm_sincos_short_p(x1, s1, c1, K);
         return;
     }
-#endif
+    /* past 1/16 (tumbling envs: in the steady state most waves hold one, so
+     * this path runs beside the short one on nearly every tick): the yaw's
+     * branch-free one-stage reduction, not fdlibm's ranges */
+    sm_sincos_yaw_p(x0, s0, c0, K);
+    sm_sincos_yaw_p(x1, s1, c1, K);
+#else
     sm_sincos_p(x0, s0, c0, K);
     sm_sincos_p(x1, s1, c1, K);
+#endif
 }
 /* sin / cos of the yaw (any size: the heading is uniform over the circle).
  * fdlibm's reduction and kernels, streamlined for a SIMD lane (every step is

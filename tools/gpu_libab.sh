@@ -13,6 +13,6 @@ for r in $(seq ${ROUNDS:-2}); do
         l=$lib; [ "$lib" = product ] && l=""
         SALP_LIB=$l timeout -k 10 180 python bench.py --steps ${STEPS:-8} --warmup 1 --no-cpu-baseline --no-parity-check \
             > gpurun_out/ab.log 2>&1 || { tail -n 5 gpurun_out/ab.log; exit 1; }
-        python -c "import json;d=json.loads(open('gpurun_out/ab.log').read().strip().splitlines()[-1]);print('$lib', round(d['value']/1e6,3), round(d['lockstep_env_steps_per_sec']/1e6,3), d['kernel_ms_per_launch'])"
+        python -c "import json;d=json.loads(open('gpurun_out/ab.log').read().strip().splitlines()[-1]);print('$lib', round(d['value']/1e6,3), round(d['lockstep_env_steps_per_sec']/1e6,3), d['kernel_ms_per_launch'], round(d.get('steady_state_env_steps_per_sec') or 0, -5)/1e6)"
     done
 done
