@@ -172,16 +172,32 @@ def load(path=LIB_PATH):
         raise SalpError(f"{path} not found: build it with `python -m grasp_lab_salp_amd.build` "
                         "(there is no CPU fallback for the simulator)")
     L = ctypes.CDLL(path)
-    # SALP_AB_OLD_ABI=1: an A/B run against a library of an earlier round (its
-    # missing newer entry points stay unbound, its older ABI number passes);
-    # the state and trace layouts must still match
-    old_ok = os.environ.get("SALP_AB_OLD_ABI") == "1"
+    # SALP_AB_OLD_ABI=1: an A/B run (tools/gpu_*_ab.sh) against a library of an
+    # earlier round -- its older ABI number passes and its missing newer entry
+    # points stay unbound.  Only for an explicit SALP_LIB other than the
+    # in-tree build, never silently: it warns, and the PPO paths that need a
+    # newer entry point are switched to their older equivalents (a library
+    # without salp_ppo_mlp_adv_partials gets SALP_PPO_EPOCH_ADV=0).  The state
+    # and trace layouts must still match.
+    old_ok = (os.environ.get("SALP_AB_OLD_ABI") == "1" and bool(os.environ.get("SALP_LIB"))
+              and os.path.abspath(path) != os.path.join(HERE, "libsalp.so"))
+    if os.environ.get("SALP_AB_OLD_ABI") == "1" and not old_ok:
+        raise SalpError("SALP_AB_OLD_ABI=1 is for A/B runs of another library: set SALP_LIB to it")
+    missing = []
     for name, (res, args) in SIGNATURES.items():
         if old_ok and not hasattr(L, name):
+            missing.append(name)
             continue
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
+    if old_ok:
+        import warnings
+        warnings.warn(f"SALP_AB_OLD_ABI=1: {path} loaded without the ABI check (ABI "
+                      f"{L.salp_abi_version()} vs {ABI_VERSION}; unbound: {missing or 'none'}) -- A/B use only",
+                      RuntimeWarning, stacklevel=2)
+        if "salp_ppo_mlp_adv_partials" in missing:
+            os.environ["SALP_PPO_EPOCH_ADV"] = "0"
     if L.salp_abi_version() != ABI_VERSION and not old_ok:
         raise SalpError("libsalp ABI version mismatch")
     if L.salp_num_fields() != NUM_FIELDS:

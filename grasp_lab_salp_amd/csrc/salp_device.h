@@ -437,6 +437,16 @@ struct Hot {
     uint64_t env_id;
 };
 
+/* An env whose two-wave cycle could not finish (a partner wait gave up): its
+ * motion state becomes NaN, the state a diverged env carries. */
+SD_HOST_DEV void poison_motion(Hot& h) {
+    const double nan = __builtin_nan("");
+    h.v0 = h.v1 = h.v2 = h.w0 = h.w1 = h.w2 = nan;
+    h.a0 = h.a1 = h.a2 = h.al0 = h.al1 = h.al2 = nan;
+    h.e0 = h.e1 = h.e2 = h.p0 = h.p1 = h.p2 = nan;
+    h.sp = h.cp = h.st = h.cth = nan;
+}
+
 /* Fields store_hot writes (the tick's state); every other field is "cold":
  * touched only at env-step boundaries.  RAND kernels also carry Hot::Rnd. */
 SD_HOST_DEV constexpr bool is_rnd(int f) {

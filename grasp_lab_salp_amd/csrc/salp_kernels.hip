@@ -1126,7 +1126,7 @@ __device__ __forceinline__ void pair_publish(int* flag, int value) {
 // wave 1) with its two counters, and wave 1's hand-over of the angle chain.
 constexpr int kWaveRing = 64;                       // ticks wave 0 may run ahead
 enum { WR_V0, WR_V1, WR_V2, WR_W0, WR_W1, WR_W2, WR_STRIDE = 6 };
-enum { WX_E0, WX_E1, WX_E2, WX_P0, WX_P1, WX_P2, WX_SP, WX_CP, WX_ST, WX_CTH, WX_N };
+enum { WX_E0, WX_E1, WX_E2, WX_P0, WX_P1, WX_P2, WX_SP, WX_CP, WX_ST, WX_CTH, WX_FAIL, WX_N };
 struct WaveShared {
     double rows[kWave * WG_STRIDE];
     double ring[kWaveRing * WR_STRIDE];
@@ -1228,7 +1228,7 @@ __global__ __launch_bounds__(2 * kWave) void k_step_wave(double* S, Params P, co
         if (!kin) salp::store_cold<RAND>(C, S, P, i);
     }
     __syncthreads();
-    run_cycle_split<RAND>(h, P, c32, W);
+    const bool ok = run_cycle_split<RAND>(h, P, c32, W);
     __syncthreads();
     if (kin) {
         if (threadIdx.x == kWave) {
@@ -1236,6 +1236,7 @@ __global__ __launch_bounds__(2 * kWave) void k_step_wave(double* S, Params P, co
             x[WX_E0] = h.e0; x[WX_E1] = h.e1; x[WX_E2] = h.e2;
             x[WX_P0] = h.p0; x[WX_P1] = h.p1; x[WX_P2] = h.p2;
             x[WX_SP] = h.sp; x[WX_CP] = h.cp; x[WX_ST] = h.st; x[WX_CTH] = h.cth;
+            x[WX_FAIL] = ok ? 0.0 : 1.0;
         }
     }
     __syncthreads();
@@ -1245,6 +1246,12 @@ __global__ __launch_bounds__(2 * kWave) void k_step_wave(double* S, Params P, co
         h.e0 = x[WX_E0]; h.e1 = x[WX_E1]; h.e2 = x[WX_E2];
         h.p0 = x[WX_P0]; h.p1 = x[WX_P1]; h.p2 = x[WX_P2];
         h.sp = x[WX_SP]; h.cp = x[WX_CP]; h.st = x[WX_ST]; h.cth = x[WX_CTH];
+        /* a partner wait that gave up (g_pair_timeouts counted it) leaves this env's
+         * cycle unfinished: its state is not the reference's, so mark it invalid
+         * rather than hand it on as a result -- NaN motion state, which every
+         * caller already treats as a diverged env (NaN obs and reward, the
+         * learner's divergence guard resets it, salp_pair_timeouts says why) */
+        if (!ok || x[WX_FAIL] != 0.0) salp::poison_motion(h);
     }
     float o[SALP_OBS_DIM_MAX];
     double* info = info_out ? info_out + (size_t)SALP_INFO_DIM * i : nullptr;

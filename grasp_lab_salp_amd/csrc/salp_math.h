@@ -204,7 +204,13 @@ SM_QUAL int sm_rem_pio2_p(double x, double* y0, double* y1, SmPoly K) {
                  pio2_2 = 6.07710050630396597660e-11, pio2_2t = 2.02226624879595063154e-21,
                  pio2_3 = 2.02226624871116645580e-21, pio2_3t = 8.47842766036889956997e-32;
     double fn = rint(x * invpio2);
-    double r = sm_mad(-fn, pio2_1, x);   /* fn * pio2_1 is exact (33-bit pio2_1): same either way */
+    /* fn * pio2_1 is exact while |fn| < 2^20 (33-bit pio2_1), so the unfused
+     * and the fused form agree there; beyond (|x| > 1.6e6, tumbling or
+     * diverging envs) only the fused one keeps the product exact, and the
+     * unfused one lost ~ulp(x) of the angle (NumPy mode 1e-5 off the
+     * reference at 1e10 rad, tests/test_oracle_tumble.py).  Fused in both
+     * modes: this is libm's reduction, not a NumPy expression. */
+    double r = sm_fma(-fn, pio2_1, x);
     double w = fn * pio2_1t;
     double y = r - w;
     int j = (sm_hi(x) >> 20) & 0x7ff;
@@ -230,8 +236,10 @@ SM_QUAL int sm_rem_pio2_p(double x, double* y0, double* y1, SmPoly K) {
      * (and saturates on the GPU) once |fn| >= 2^31, which a diverged env's
      * angle reaches (UBSan, tools/sanitize).  Callers only use n & 3; for
      * |fn| < 2^31 this is exactly (int)fn & 3.  (Beyond |x| = 2^20 pi/2 the
-     * medium-case reduction is inexact, as in fdlibm's medium branch; such
-     * angles only occur in envs whose state already diverged.) */
+     * later stages' products are no longer exact, so the reduction loses
+     * its guarantee, as fdlibm's medium branch does where fdlibm switches to
+     * Payne-Hanek; measured against the reference up to 1e11 rad it stays
+     * within the tumble fixtures' tolerances.) */
     const double q = fn - 4.0 * floor(fn * 0.25);
     return q == q ? (int)q : 0;
 }
@@ -336,9 +344,16 @@ SM_QUAL void sm_sincos_rp2(double x0, double x1, double* s0, double* c0, double*
  *    fn is in the low bits of x 2/pi + 1.5 * 2^52 (exact for |fn| < 2^51);
  *  - one Cody-Waite stage (pio2_1, pio2_1t).  fdlibm adds a second and third
  *    stage when more than 16 bits cancel (x within |x| 2^-16 of a multiple of
- *    pi/2); the first stage's absolute error is below |fn| 1e-26, so the
- *    result stays within one ulp unless |y| < |fn| 1e-10, and within 1e-26
- *    absolute always;
+ *    pi/2); the fused first stage keeps fn * pio2_1 exact for every fn, so
+ *    the absolute error is below 1.5e-26 |fn| (pio2_1t's own truncation):
+ *    within one ulp unless |y| < |fn| 1e-10 for |x| <= 2^20 pi/2, within
+ *    1.5e-26 |fn| + ulp(1) up to |x| < 2^51 pi/2 (~3.5e15).  Beyond that the
+ *    magic-add quadrant breaks and the result is not sin / cos (values up
+ *    to 1e176, NaN from ~1e100): only an env whose state is already
+ *    diverging gets there (finite angles seen: <= 3.9e11), the device still
+ *    equals the oracle, and the reference's pin reaches 1e11 rad
+ *    (tests/test_math.py test_tick_yaw_sincos_large_angles,
+ *    tests/test_oracle_tumble.py);
  *  - the tail forms of the kernels for every argument (y1 = 0 when fn = 0);
  *  - quadrant swap as selects, the two signs as bit flips.
  * Differs from sm_sincos_p by at most an ulp. */
@@ -348,7 +363,7 @@ SM_QUAL void sm_sincos_yaw_p(double x, double* s_out, double* c_out, SmPoly K) {
     const double t = x * K.R_INV + magic;
     const double fn = t - magic;
     const uint32_t q = (uint32_t)sm_d2u(t) & 3u;
-    const double r = sm_mad(-fn, K.R_P1, x);   /* fn * pio2_1 is exact (33-bit pio2_1) */
+    const double r = sm_mad(-fn, K.R_P1, x);   /* the fused product is exact for every fn */
     const double w = fn * K.R_P1T;
     const double y0 = r - w;
     const double y1 = (r - y0) - w;

@@ -240,6 +240,9 @@ int salp_set_rollout_kernel(SalpEnv* h, int mode);
  * launch are then invalid.  Reads (synchronising `stream`) and clears the
  * count of such waits since the previous call, over every launch of the
  * process; 0 is the only good answer (the Python layer raises otherwise).
+ * k_step_wave (salp_step) also marks such an env invalid in place: its motion
+ * state is set to NaN, the state of a diverged env, so a caller that never
+ * reads this count still cannot take the unfinished cycle for a result.
  * Diagnostic with no reference counterpart. */
 int salp_pair_timeouts(SalpEnv* h, uint64_t* count_out, void* stream);
 /* Kernel of salp_step (ABI 11): -1 auto (default), 0 one env per lane

@@ -71,7 +71,11 @@ def test_device_math_equals_oracle_math():
     # the tick's roll / pitch pair: both short, one short, either NaN / inf
     xs = np.concatenate([rng.uniform(-0.07, 0.07, 8000), [0.0, -0.0, 0.0625, -0.0625, np.nan, 0.01, np.inf, 0.01]])
     ys = np.concatenate([rng.uniform(-0.07, 0.07, 8000), [0.0, 0.0, 0.0625, 0.07, 0.01, np.nan, 0.01, -np.inf]])
-    x, y = np.concatenate([x, xs]), np.concatenate([y, ys])
+    # tumbling and diverging angles: the medium range, up to 2^51 pi/2, and
+    # beyond it where sm_sincos_yaw_p is unspecified (tests/test_math.py) but
+    # the device must still equal the oracle
+    big = 10.0 ** rng.uniform(1, 308, 4000) * rng.choice([-1.0, 1.0], 4000)
+    x, y = np.concatenate([x, xs, big]), np.concatenate([y, ys, big[::-1]])
     from grasp_lab_salp_amd import _lib
     import ctypes
     L = _lib.load()

@@ -130,6 +130,46 @@ def test_tick_yaw_sincos_within_one_ulp():
     assert np.isnan(nan[12]).all() and np.isnan(nan[13]).all()
 
 
+def test_tick_yaw_sincos_large_angles():
+    """sm_sincos_yaw_p past a few turns — the range tumbling envs' roll and
+    pitch reach (up to 1e5 rad in the bench's steady state, a finite 3.9e11
+    during one blow-up: profiles/r5am_angle_census.json).  What it
+    guarantees, against mpmath at 300 bits:
+
+    * |x| <= 2^20 pi/2 (fdlibm's medium range, |fn| < 2^20): within one ulp,
+      except where the result is within 1e-10 |fn| of zero (the single
+      Cody-Waite stage, as above);
+    * |x| < 2^51 pi/2 (~3.5e15; the magic-add quadrant is exact for
+      |fn| < 2^51): absolute error <= 1.5e-26 |fn| + one ulp of 1 (the fused
+      first stage keeps fn * pio2_1 exact; what is left is pio2_1t's own
+      truncation, |fn| * 2^-87);
+    * beyond: unspecified — not sin / cos at all (|values| up to 1e176, NaN
+      from ~1e100 rad), reached only by envs whose state is already
+      diverging; device == oracle there still holds bit for bit (shared code,
+      the GPU math self-test).  The reference's own pin up to 1e11 rad is
+      tests/test_oracle_tumble.py."""
+    rng = np.random.default_rng(11)
+    med = 2.0 ** 20 * math.pi / 2
+    big = 2.0 ** 51 * math.pi / 2
+    k = rng.integers(1, 2 ** 20, 1500) * rng.choice([-1, 1], 1500)
+    x1 = np.concatenate([10.0 ** rng.uniform(1.5, math.log10(med), 3000) * rng.choice([-1, 1], 3000),
+                         k * (math.pi / 2) + rng.uniform(-1e-4, 1e-4, len(k))])
+    x1 = x1[np.abs(x1) <= med]
+    x2 = 10.0 ** rng.uniform(math.log10(med), math.log10(big) - 0.01, 3000) * rng.choice([-1, 1], 3000)
+    with mpmath.workprec(300):
+        for x, bound in ((x1, "ulp"), (x2, "abs")):
+            out = oracle.math_selftest(x, np.zeros_like(x))
+            fn = np.abs(np.rint(x * 2 / math.pi))
+            for row, f in ((12, mpmath.sin), (13, mpmath.cos)):
+                exact = np.array([float(f(mpmath.mpf(float(v)))) for v in x])
+                err = np.abs(out[row] - exact)
+                assert np.all(err <= 1.5e-26 * fn + np.spacing(1.0)), (row, bound, float(np.max(err)))
+                if bound == "ulp":
+                    ok = np.abs(exact) > 1e-10 * fn
+                    e = ulp_err(out[row][ok], exact[ok])
+                    assert np.max(e) <= 1.0, (row, float(np.max(e)))
+
+
 def test_tick_roll_pitch_pair():
     """sm_sincos_rp2: the four-term kernels when neither |angle| exceeds 1/16
     (or is NaN), within one ulp; the yaw's one-stage function for both

@@ -69,6 +69,7 @@ def main():
     ap.add_argument("--lockstep-order", type=int, default=-1, help="salp_set_lockstep_order mode")
     ap.add_argument("--collect", default="auto", choices=("auto", "lockstep", "chained"),
                     help="collection: salp_step per env-step, or salp_collect (policy inside the kernel)")
+    ap.add_argument("--no-graphs", action="store_true", help="eager minibatch steps (PPO(use_graphs=False))")
     ap.add_argument("--recurrent", action="store_true",
                     help="RecurrentPPO with the MlpLstmPolicy (LSTM 256) of src/train_robot_recurrent_ppo.py")
     ap.add_argument("--lstm-hidden", type=int, default=256)
@@ -91,7 +92,7 @@ def main():
                              seed=0, seq_len=a.seq_len, policy_kwargs={"lstm_hidden_size": a.lstm_hidden})
     else:
         model = PPO("MlpPolicy", env, n_steps=a.n_steps, batch_size=a.batch_size, n_epochs=a.n_epochs, seed=0,
-                    collect=a.collect)
+                    collect=a.collect, use_graphs=False if a.no_graphs else None)
     # warm-up (+ trend) iterations, one learn() call each so that a long trend
     # reports progress on stderr (a GPU job silent for minutes looks hung)
     for it in range(max(1, a.trend_iters)):
