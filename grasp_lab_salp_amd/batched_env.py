@@ -188,9 +188,10 @@ class BatchedSalpEnv:
     def set_rollout_kernel(self, mode):
         """Kernel of :meth:`rollout`, :meth:`collect` and chained
         :meth:`step_random` (salp_set_rollout_kernel): 1 = two waves per env
-        (k_rollout_pair), 0 = one env per lane (k_rollout), -1 = the pair
-        kernel up to 128 envs per compute unit (default).  Results are
-        identical in every mode."""
+        meeting once per tick (k_rollout_pair), 2 = two waves per env with the
+        tick split one way (k_rollout_split), 0 = one env per lane (k_rollout),
+        -1 = a two-wave kernel up to 128 envs per compute unit (default).
+        Results are identical in every mode."""
         self._check(_lib.load().salp_set_rollout_kernel(self._h, int(mode)))
 
     def set_step_kernel(self, mode):

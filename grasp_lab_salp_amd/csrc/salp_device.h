@@ -866,7 +866,10 @@ SD void tick_dynamics(Hot& h, const Params& P, double* rec, int64_t rs) {
  * skipped.  Every remaining operation is the same, so the results are bit
  * for bit those of the plain steady tick; and the tick ends settled again.
  * Returns, for a STEADY tick, whether this lane is settled after it. */
-template <bool REC = false, bool RAND = false, bool LATE32 = false, bool STEADY = false, bool SETTLED = false>
+/* PARTS: the tick_dynamics parts this tick runs (k_rollout_split's A wave runs
+ * TD_FORCES | TD_POSITIONS and leaves TD_KINEMATICS to its B wave). */
+template <bool REC = false, bool RAND = false, bool LATE32 = false, bool STEADY = false, bool SETTLED = false,
+          int PARTS = TD_ALL>
 SD bool tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_t rs = 0) {
     static_assert(!SETTLED || STEADY, "a settled tick is a steady one");
     /* this cycle's float32-mode geometry, used at the end if the lane is in
@@ -874,7 +877,7 @@ SD bool tick(Hot& h, const Params& P, Cache32 c32, double* rec = nullptr, int64_
     double k32[C32_N];
     if (!LATE32 && !STEADY)
         for (int k = 0; k < C32_N; ++k) k32[k] = c32[k];
-    tick_dynamics<REC, RAND, SETTLED>(h, P, rec, rs);
+    tick_dynamics<REC, RAND, SETTLED, PARTS>(h, P, rec, rs);
     /* ---------------- clocks, phase, properties ---------------- */
     h.ct += DT;
     h.time += DT;

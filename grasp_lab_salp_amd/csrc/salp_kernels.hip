@@ -1389,7 +1389,23 @@ __device__ __forceinline__ void pair_reseat(PairShared& sh, int b, int seat, int
     steps = sh.steps[s];
 }
 
-template <bool POL>
+// k_rollout_split (SPLIT): the same workgroup, slots, re-seating and
+// boundaries as k_rollout_pair, but the tick is split along its one-way
+// dependences instead of Newton <-> Euler: the A wave runs whole ticks without
+// the angle chain (tick<..., TD_FORCES | TD_POSITIONS>: forces, v / w
+// integration, clock, phase, geometry, the steady / settled decisions), and
+// the B wave follows with the angle chain (TD_KINEMATICS: Euler-angle rates,
+// angles, their sin / cos, the world-frame position), which nothing the A wave
+// computes reads.  Per wave-tick the A wave writes every lane's v and w into an
+// LDS ring of kSplitRing ticks; it waits only when the B wave is a whole ring
+// behind, so there is no per-tick round trip.  Each value is the expression
+// tick() computes: results equal k_rollout's and the oracle's bit for bit.
+constexpr int kSplitRing = 8;            // wave-ticks the A wave may run ahead
+constexpr int kSplitEnd = 1 << 30;       // the A wave's counter: end of its chunk
+static_assert(2 * kSplitRing * 6 * 64 <= salp::SPILL_N * kPairEnvs, "the rings live in the spill slots' LDS");
+constexpr int kSplitParts = salp::TD_FORCES | salp::TD_POSITIONS;
+
+template <bool POL, bool SPLIT = false>
 __device__ __forceinline__ void pair_wave_a(PairShared& sh, PairJobs* jobs, const RolloutArgs& A, int grp, int lane) {
     const Params& P = A.P;
     const int seat = grp * 64 + lane;
@@ -1482,6 +1498,74 @@ __device__ __forceinline__ void pair_wave_a(PairShared& sh, PairJobs* jobs, cons
         if (all_done) continue;
         const salp::SpillSlot ns{sh.big + s, kPairEnvs};
         const salp::Cache32 c32{sh.cache32 + s, kPairEnvs};
+        if constexpr (SPLIT) {
+            Hot h;
+            salp::unspill<false>(h, ns, P, (uint64_t)(P.env_offset + i));
+            if (!active) h.b2 = -INFINITY;
+            prof.lap(PP_BOUNDARY);
+            __syncthreads();   // #2: slots read; the ring may overwrite them now
+            prof.lap(PP_BARRIER);
+            {
+                const Params PV = salp::pin_params(P);
+                double2* const ring = reinterpret_cast<double2*>(sh.big) + grp * kSplitRing * 3 * 64 + lane;
+                int g = 0;           // wave-ticks published
+                int freed = kSplitRing;   // slots below this count are free (the B wave read them)
+                bool ok = true;
+                const auto publish = [&]() {
+                    if (g >= freed) {
+                        prof.lap(PP_TICK);
+                        const int want = g - kSplitRing + 1;
+                        ok = pair_wait(&sh.cnt[grp][1], want) && ok;
+                        freed = __hip_atomic_load(&sh.cnt[grp][1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) +
+                                kSplitRing;
+                        freed = freed > g ? freed : g + 1;
+                        prof.lap(PP_WAIT);
+                    }
+                    double2* const q = ring + (g % kSplitRing) * 3 * 64;
+                    q[0] = make_double2(h.v0, h.v1);
+                    q[64] = make_double2(h.v2, h.w0);
+                    q[128] = make_double2(h.w1, h.w2);
+                    pair_publish(&sh.cnt[grp][0], ++g);
+                };
+                // k_rollout's chunk: full ticks while a ticking lane is unsteady, then
+                // the steady budget (settled once every ticking lane is)
+                int32_t k = 0;
+                for (; k < A.chunk && ok; ++k) {
+                    if (__all(!(h.ct < h.b2) || salp::next_tick_steady(h, PV))) break;
+                    if (h.ct < h.b2) salp::tick<false, false, true, false, false, kSplitParts>(h, PV, c32);
+                    publish();
+                }
+                const int32_t ks = (int32_t)(((int64_t)(A.chunk - k) * A.steady_q8) >> 8);
+                int32_t j = 0;
+                for (; j < ks && ok; ++j) {
+                    bool settled = true;
+                    if (h.ct < h.b2) settled = salp::tick<false, false, true, true, false, kSplitParts>(h, PV, c32);
+                    publish();
+                    if (__all(settled)) {
+                        ++j;
+                        break;
+                    }
+                }
+                for (; j < ks && ok; ++j) {
+                    if (h.ct < h.b2) salp::tick<false, false, true, true, true, kSplitParts>(h, PV, c32);
+                    publish();
+                }
+                pair_publish(&sh.cnt[grp][0], g | kSplitEnd);
+                prof.lap(PP_TICK);
+            }
+            __syncthreads();   // #3: the B wave has read the ring
+            prof.lap(PP_BARRIER);
+            if (lane == 0) {   /* the next chunk counts from 0 (neither wave reads them before #2) */
+                sh.cnt[grp][0] = 0;
+                sh.cnt[grp][1] = 0;
+            }
+            salp::spill<false>(h, ns);   // the angle chain's fields are stale here: the B wave's follow
+            __syncthreads();   // #3b
+            prof.lap(PP_BOUNDARY);
+            __syncthreads();   // #4: slots whole again
+            prof.lap(PP_BARRIER);
+            continue;
+        }
         salp::HotA h;
         salp::unspill_a(h, ns);
         if (!active) h.b2 = -INFINITY;
@@ -1566,7 +1650,7 @@ __device__ __forceinline__ void pair_wave_a(PairShared& sh, PairJobs* jobs, cons
     }
 }
 
-template <bool POL>
+template <bool POL, bool SPLIT = false>
 __device__ __forceinline__ void pair_wave_b(PairShared& sh, PairJobs* jobs, const RolloutArgs& A, int grp, int lane) {
     const Params& P = A.P;
     const int seat = grp * 64 + lane;
@@ -1602,6 +1686,55 @@ __device__ __forceinline__ void pair_wave_b(PairShared& sh, PairJobs* jobs, cons
         if (all_done) continue;
         const salp::SpillSlot ns{sh.big + s, kPairEnvs};
         const salp::Cache32 c32{sh.cache32 + s, kPairEnvs};
+        if constexpr (SPLIT) {
+            Hot h;
+            salp::unspill<false>(h, ns, P, 0);
+            if (!active) h.b2 = -INFINITY;
+            prof.lap(PP_BOUNDARY);
+            __syncthreads();   // #2
+            prof.lap(PP_BARRIER);
+            {
+                const Params PV = salp::pin_params(P);
+                const double2* const ring = reinterpret_cast<const double2*>(sh.big) + grp * kSplitRing * 3 * 64 + lane;
+                for (int g = 0;; ++g) {
+                    // wait for wave-tick g, or the end of the chunk before it
+                    int c = 0;
+                    for (int it = 0;; ++it) {
+                        c = __hip_atomic_load(&sh.cnt[grp][0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if ((c & ~kSplitEnd) > g || (c & kSplitEnd)) break;
+                        if (it >= kPairSpin) {   /* give up: this chunk's results are invalid */
+                            if (lane == 0) atomicAdd(&g_pair_timeouts, 1u);
+                            c = g | kSplitEnd;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    prof.lap(PP_WAIT);
+                    if ((c & ~kSplitEnd) <= g) break;
+                    const double2* const q = ring + (g % kSplitRing) * 3 * 64;
+                    const double2 x0 = q[0], x1 = q[64], x2 = q[128];
+                    pair_publish(&sh.cnt[grp][1], g + 1);   // slot read: the A wave may refill it
+                    prof.lap(PP_READ);
+                    if (h.ct < h.b2) {
+                        h.v0 = x0.x; h.v1 = x0.y; h.v2 = x1.x; h.w0 = x1.y; h.w1 = x2.x; h.w2 = x2.y;
+                        salp::tick_dynamics<false, false, false, salp::TD_KINEMATICS>(h, PV, nullptr, 0);
+                        h.ct += salp::DT;
+                    }
+                    prof.lap(PP_TICK);
+                }
+            }
+            __syncthreads();   // #3
+            prof.lap(PP_BARRIER);
+            __syncthreads();   // #3b: the A wave spilled its fields
+            prof.lap(PP_BARRIER);
+            ns[salp::SP_E] = h.e0; ns[salp::SP_E + 1] = h.e1; ns[salp::SP_E + 2] = h.e2;
+            ns[salp::SP_P] = h.p0; ns[salp::SP_P + 1] = h.p1; ns[salp::SP_P + 2] = h.p2;
+            ns[salp::SP_SP] = h.sp; ns[salp::SP_CP] = h.cp; ns[salp::SP_ST] = h.st; ns[salp::SP_CTH] = h.cth;
+            prof.lap(PP_BOUNDARY);
+            __syncthreads();   // #4
+            prof.lap(PP_BARRIER);
+            continue;
+        }
         salp::HotB h;
         salp::unspill_b(h, ns, P);
         if (!active) h.b2 = -INFINITY;
@@ -1675,6 +1808,23 @@ __global__ __launch_bounds__(kBlock) void k_rollout_pair(RolloutArgs A) {
     }
     if (wave & 1) pair_wave_b<POL>(sh, jobs, A, wave >> 1, lane);
     else pair_wave_a<POL>(sh, jobs, A, wave >> 1, lane);
+}
+
+// k_rollout_split: k_rollout_pair's workgroup with the tick split one way
+// (pair_wave_a / pair_wave_b, SPLIT).
+template <bool POL>
+__global__ __launch_bounds__(kBlock) void k_rollout_split(RolloutArgs A) {
+    __shared__ PairShared sh;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = (int)(threadIdx.x & 63);
+    PairJobs* const jobs = pair_jobs_lds<POL>();
+    if (POL) {   /* the actor's second layer into LDS, once per workgroup */
+        const float* src = (const float*)A.R.weights + SALP_POLICY_PI_W2;
+        for (int k = (int)threadIdx.x; k < kPolL2; k += kBlock) jobs->pi_l2[k] = src[k];
+        __syncthreads();
+    }
+    if (wave & 1) pair_wave_b<POL, true>(sh, jobs, A, wave >> 1, lane);
+    else pair_wave_a<POL, true>(sh, jobs, A, wave >> 1, lane);
 }
 
 // The ABI's field-major state (state[f * n + i]) <-> the handle's layout
@@ -1837,7 +1987,7 @@ struct SalpEnv {
     void* sort_temp = nullptr;
     size_t sort_temp_bytes = 0;
     int64_t* step_counts = nullptr;   // per-env env-step counter of a chained salp_step_random
-    int rollout_kernel = -1;          // salp_set_rollout_kernel: -1 auto, 0 k_rollout, 1 k_rollout_pair
+    int rollout_kernel = -1;          // salp_set_rollout_kernel: -1 auto, 0 k_rollout, 1 k_rollout_pair, 2 k_rollout_split
     int step_kernel = -1;             // salp_set_step_kernel: -1 auto, 0 k_step, 1 k_step_wave
     int cu_count = 256;               // compute units of the device (the auto choice)
 };
@@ -1914,7 +2064,7 @@ bool randomized(const Params& d) { return d.rand_dyn || d.rand_dist || d.rand_ac
 // The pair kernel has no randomised instance.
 bool use_pair(const SalpEnv* h) {
     if (randomized(h->dp)) return false;
-    if (h->rollout_kernel == 0 || h->rollout_kernel == 1) return h->rollout_kernel == 1;
+    if (h->rollout_kernel >= 0) return h->rollout_kernel >= 1;
     static const int forced = [] {
         const char* e = std::getenv("SALP_ROLLOUT_KERNEL");
         return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
@@ -1923,6 +2073,36 @@ bool use_pair(const SalpEnv* h) {
     return h->n <= (int64_t)h->cu_count * 128;
 }
 unsigned pair_blocks_for(int64_t n) { return (unsigned)((n + kPairEnvs - 1) / kPairEnvs); }
+// Of the two-wave kernels: the one-way split (k_rollout_split) in mode 2, the
+// Newton <-> Euler pair in mode 1; the auto choice's two-wave kernel is the
+// pair unless SALP_TWO_WAVE_KERNEL=split (A/B runs).
+bool use_split(const SalpEnv* h) {
+    if (h->rollout_kernel >= 1) return h->rollout_kernel == 2;
+    static const bool split = [] {
+        const char* e = std::getenv("SALP_TWO_WAVE_KERNEL");
+        return e && e[0] == 's';
+    }();
+    return split;
+}
+// k_rollout_split's steady budgets (SALP_SPLIT_STEADY_Q8 / SALP_SPLIT_COLLECT_Q8
+// override them): its steady ticks lose the angle chain as its full ones do,
+// so k_rollout's ratio is the starting point.
+int32_t split_steady_q8() {
+    static const int32_t q = [] {
+        const char* e = std::getenv("SALP_SPLIT_STEADY_Q8");
+        const long v = e ? std::strtol(e, nullptr, 10) : 0;
+        return (int32_t)(v > 0 && v < (1 << 16) ? v : 560);
+    }();
+    return q;
+}
+int32_t split_collect_steady_q8() {
+    static const int32_t q = [] {
+        const char* e = std::getenv("SALP_SPLIT_COLLECT_Q8");
+        const long v = e ? std::strtol(e, nullptr, 10) : 0;
+        return (int32_t)(v > 0 && v < (1 << 16) ? v : 560);
+    }();
+    return q;
+}
 
 // salp_step's kernel: one wave per env (k_step_wave) for small batches - the
 // per-env SalpRobotEnv and small vector envs, where a lane per env leaves the
@@ -1940,6 +2120,12 @@ bool use_step_wave(const SalpEnv* h) {
 int launch_chained(SalpEnv* h, const RolloutArgs& args, bool pol, hipStream_t st, const char* what) {
     if (use_pair(h)) {
         RolloutArgs pa = args;
+        if (use_split(h)) {
+            pa.steady_q8 = pol ? split_collect_steady_q8() : split_steady_q8();
+            hipLaunchKernelGGL(pol ? k_rollout_split<true> : k_rollout_split<false>, dim3(pair_blocks_for(h->n)),
+                               dim3(kBlock), 0, st, pa);
+            return launched(h, what);
+        }
         pa.steady_q8 = pol ? pair_collect_steady_q8() : pair_steady_q8();
         hipLaunchKernelGGL(pol ? k_rollout_pair<true> : k_rollout_pair<false>, dim3(pair_blocks_for(h->n)),
                            dim3(kBlock), 0, st, pa);
@@ -2358,7 +2544,7 @@ int salp_set_step_kernel(SalpEnv* h, int mode) {
 
 int salp_set_rollout_kernel(SalpEnv* h, int mode) {
     if (!h) return fail(nullptr, SALP_EINVAL, "salp_set_rollout_kernel: null handle");
-    if (mode < -1 || mode > 1) return fail(h, SALP_EINVAL, "salp_set_rollout_kernel: mode must be -1, 0 or 1");
+    if (mode < -1 || mode > 2) return fail(h, SALP_EINVAL, "salp_set_rollout_kernel: mode must be -1, 0, 1 or 2");
     h->rollout_kernel = mode;
     return SALP_OK;
 }

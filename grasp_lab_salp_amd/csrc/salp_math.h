@@ -299,43 +299,23 @@ SM_QUAL void sm_sincos(double x, double* s_out, double* c_out) { sm_sincos_p(x, 
  * the oracle stays inside the golden tolerances against the reference's own
  * NumPy (glibc) sin / cos (tests/test_oracle_golden.py). */
 
-/* Roll and pitch stay small (|x| < 1/16 for 99.996 % of the ticks of a
- * random-action run; oracle, 4 096 envs x 120 env-steps): there fdlibm's
- * degree-13 / 14 kernels need only their first four terms (the dropped
- * S5 x^11 and C5 x^12 are below 2^-60 relative).  sin x = x + x^3 (S1 + z S2
- * + z^2 S3 + z^3 S4), cos x = w + (((1 - w) - z/2) + z r) with w = 1 - z/2 and
- * r = z (C1 + z C2 + z^2 C3 + z^3 C4), z = x^2 (fdlibm's own cos form). */
-#define SM_SHORT_MAX 0.0625
-SM_QUAL void sm_sincos_short_p(double x, double* s_out, double* c_out, SmPoly K) {
-    const double z = x * x;
-    *s_out = sm_mad(z * x, sm_mad(z, sm_mad(z, sm_mad(z, K.S4, K.S3), K.S2), K.S1), x);
-    const double r = z * sm_mad(z, sm_mad(z, sm_mad(z, K.C4, K.C3), K.C2), K.C1);
-    const double hz = 0.5 * z, w = 1.0 - hz;
-    *c_out = w + sm_mad(z, r, (1.0 - w) - hz);
-}
-/* sin / cos of roll x0 and pitch x1 together: the short kernels for both when
- * neither |x| exceeds 1/16 (NaN included: the kernels return NaN for it, and a
- * diverged env's NaN angles do not send its wave down the long path), else
- * the yaw's sm_sincos_yaw_p for both (fdlibm's sm_sincos_p without
- * SALP_FMA).  The choice is a function of (x0, x1) alone
- * (per lane, not per wave), so results do not depend on the other lanes. */
+/* sin / cos of roll x0 and pitch x1 together (round 6): the yaw's
+ * branch-free sm_sincos_yaw_p for both, whatever their size (fdlibm's
+ * sm_sincos_p without SALP_FMA).  Round 5 ran fdlibm's first four kernel terms
+ * while both |x| <= 1/16 and the yaw's function otherwise; in the steady state ~4 %
+ * of the envs tumble (|roll| or |pitch| > 1/16) and they sit in ~965 of 1 024
+ * waves (profiles/r5am_angle_census.json), so nearly every wave ran both
+ * paths.  One path for every lane: +12 % steady state on the headline
+ * (profiles/r5_experiments.md r5ao).  r5ao's split-invariance failure was NaN
+ * signs only: a diverged lane's NaN carries a sign bit that depends on which
+ * tick instance (full / steady / settled: negation modifiers on other
+ * operands) the lane ran, i.e. on its wave; every value that is not NaN is
+ * identical (profiles/r6c_split_probe_r5ao.json), and NaN signs and payloads
+ * are not part of the reference's results (tests compare NaN as NaN). */
 SM_QUAL void sm_sincos_yaw_p(double x, double* s_out, double* c_out, SmPoly K);
 SM_QUAL void sm_sincos_rp2(double x0, double x1, double* s0, double* c0, double* s1, double* c1, SmPoly K) {
-#if SALP_FMA
-    if (!(fabs(x0) > SM_SHORT_MAX || fabs(x1) > SM_SHORT_MAX)) {
-        sm_sincos_short_p(x0, s0, c0, K);
-        sm_sincos_short_p(x1, s1, c1, K);
-        return;
-    }
-    /* past 1/16 (tumbling envs: in the steady state most waves hold one, so
-     * this path runs beside the short one on nearly every tick): the yaw's
-     * branch-free one-stage reduction, not fdlibm's ranges */
     sm_sincos_yaw_p(x0, s0, c0, K);
     sm_sincos_yaw_p(x1, s1, c1, K);
-#else
-    sm_sincos_p(x0, s0, c0, K);
-    sm_sincos_p(x1, s1, c1, K);
-#endif
 }
 /* sin / cos of the yaw (any size: the heading is uniform over the circle).
  * fdlibm's reduction and kernels, streamlined for a SIMD lane (every step is

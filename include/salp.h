@@ -229,10 +229,13 @@ int salp_set_lockstep_order(SalpEnv* h, int mode);
  * from 32 env-steps on; ABI 9).  mode 0: one env per lane (k_rollout); 1: each
  * env on two waves that split its physics tick and meet once per tick through
  * LDS (k_rollout_pair: twice the waves, so an env count that leaves SIMDs idle
- * with one env per lane fills the chip); -1 (default): the pair kernel while
- * n_envs <= 128 x compute units.  The pair kernel has no randomised instance:
- * with a randomisation switch on the chained calls use k_rollout.  Results per
- * env are identical in every mode. */
+ * with one env per lane fills the chip); 2 (round 6): two waves per env with
+ * the tick split along its one-way dependences, the B wave's angle chain
+ * following the A wave's forces through an LDS ring (k_rollout_split);
+ * -1 (default): a two-wave kernel while n_envs <= 128 x compute units.  The
+ * two-wave kernels have no randomised instance: with a randomisation switch
+ * on the chained calls use k_rollout.  Results per env are identical in every
+ * mode. */
 int salp_set_rollout_kernel(SalpEnv* h, int mode);
 /* Partner waits of k_rollout_pair that gave up (ABI 10): the two waves of an
  * env meet once per tick; a wave that polls for its partner ~56 ms in vain

@@ -58,7 +58,7 @@ ALL_RAND = dict(dynamics=True, disturbances=True, actions=True, observations=Tru
 
 @pytest.mark.parametrize("n,n_steps,gamma,rand,zero_tick,kernel", [
     (300, 7, 0.99, False, False, -1), (1024, 5, 0.9, False, False, -1), (500, 6, 0.99, True, False, -1),
-    (700, 12, 0.99, False, True, 1), (700, 12, 0.99, False, True, 0)])
+    (700, 12, 0.99, False, True, 1), (700, 12, 0.99, False, True, 0), (700, 12, 0.99, False, True, 2)])
 def test_collect_replays_on_the_lockstep_path(n, n_steps, gamma, rand, zero_tick, kernel):
     """rand: every randomisation switch on (k_rollout<RAND, POL>; the twin's
     salp_step draws from the same Philox streams)."""

@@ -1,6 +1,9 @@
-"""k_rollout_pair (salp_pair.h): every env's physics tick split over two waves
-that meet once per tick through LDS.  It must give every env exactly the
-results of the one-env-per-lane k_rollout (and so of the oracle):
+"""The two-wave chained kernels: k_rollout_pair (salp_pair.h: every env's
+physics tick split over two waves that meet once per tick through LDS, kernel
+mode 1) and k_rollout_split (round 6: the tick split along its one-way
+dependences, the angle chain on the B wave behind an LDS ring, mode 2).  Each
+must give every env exactly the results of the one-env-per-lane k_rollout
+(and so of the oracle):
 
 * rollouts with a per-env step cap (each env ends at the same env-step
   boundary whatever the scheduling) on both kernels: state, rollout buffers
@@ -66,30 +69,36 @@ def _rollout(kernel, n, seed, budgets, max_steps, cap=8, params=None):
     return out
 
 
+TWO_WAVE = pytest.mark.parametrize("kernel", [1, 2], ids=["pair", "split"])
+
+
+@TWO_WAVE
 @pytest.mark.parametrize("n", [1, 200, 4096, 32768])
-def test_pair_rollout_equals_single_lane_rollout(n):
+def test_pair_rollout_equals_single_lane_rollout(n, kernel):
     steps = 6 if n <= 4096 else 3
     a = _rollout(0, n, 11, [10 ** 7], steps)
-    b = _rollout(1, n, 11, [10 ** 7], steps)
+    b = _rollout(kernel, n, 11, [10 ** 7], steps)
     assert (a["steps"] == steps).all() and (b["steps"] == steps).all()
     for k in a:
         assert _same(a[k], b[k]), k
 
 
-def test_pair_rollout_cut_into_short_launches():
+@TWO_WAVE
+def test_pair_rollout_cut_into_short_launches(kernel):
     """97-tick launches (chunk 128) end in the middle of cycles and chunks."""
     n = 1000
-    one = _rollout(1, n, 5, [10 ** 7], 5)
-    cut = _rollout(1, n, 5, [97] * 400 + [10 ** 7], 5)
+    one = _rollout(kernel, n, 5, [10 ** 7], 5)
+    cut = _rollout(kernel, n, 5, [97] * 400 + [10 ** 7], 5)
     for k in one:
         assert _same(one[k], cut[k]), k
 
 
-def test_pair_rollout_with_timeouts_and_zero_obstacles():
+@TWO_WAVE
+def test_pair_rollout_with_timeouts_and_zero_obstacles(kernel):
     p = default_params(num_obstacles=0)
     p.max_cycles = 3
     a = _rollout(0, 777, 3, [10 ** 7], 7, params=p)
-    b = _rollout(1, 777, 3, [10 ** 7], 7, params=p)
+    b = _rollout(kernel, 777, 3, [10 ** 7], 7, params=p)
     for k in a:
         assert _same(a[k], b[k]), k
 
@@ -127,10 +136,11 @@ def _collect(kernel, n, n_steps, seed=23, max_cycles=500, pol_seed=1):
     return out, start, obs0
 
 
+@TWO_WAVE
 @pytest.mark.parametrize("n,n_steps,max_cycles", [(500, 9, 3), (32768, 8, 500)])
-def test_pair_collect_equals_single_lane_collect(n, n_steps, max_cycles):
+def test_pair_collect_equals_single_lane_collect(n, n_steps, max_cycles, kernel):
     a, _, _ = _collect(0, n, n_steps, max_cycles=max_cycles)
-    b, _, _ = _collect(1, n, n_steps, max_cycles=max_cycles)
+    b, _, _ = _collect(kernel, n, n_steps, max_cycles=max_cycles)
     for k in a:
         if k == "ep_stats":   # float64 atomics: the summation order follows the scheduling
             assert np.allclose(a[k], b[k], rtol=1e-12, atol=0), (a[k], b[k])
@@ -138,8 +148,9 @@ def test_pair_collect_equals_single_lane_collect(n, n_steps, max_cycles):
             assert _same(a[k], b[k]), k
 
 
-def test_pair_collect_32768_envs_sampled_envs_replay_on_the_oracle():
-    """The auto choice at 32 768 envs is the pair kernel.  256 sampled env ids
+@pytest.mark.parametrize("kernel", [-1, 2], ids=["auto", "split"])
+def test_pair_collect_32768_envs_sampled_envs_replay_on_the_oracle(kernel):
+    """The auto choice at 32 768 envs is a two-wave kernel.  256 sampled env ids
     (the first and last workgroup's seats included) are replayed on the C
     oracle from their state before the call, stepping with the clipped actions
     the kernel recorded, resetting where the kernel's divergence guard did
@@ -148,7 +159,7 @@ def test_pair_collect_32768_envs_sampled_envs_replay_on_the_oracle():
     be the oracle's bit for bit (float32 rewards: rows without a timeout
     bootstrap)."""
     n, T = 32768, 24
-    out, start, obs0 = _collect(-1, n, T)
+    out, start, obs0 = _collect(kernel, n, T)
     p = default_params()
     rng = np.random.default_rng(0)
     ids = np.unique(np.concatenate([np.arange(64), np.arange(n - 64, n), rng.choice(n, 128, replace=False)]))

@@ -114,6 +114,17 @@ def test_reference_blowup_from_its_reset_state(tumble, kernel):
     assert_bits_equal(env.get_state(), torch.tensor(o.state), "blow-up", nan_payloads=True)
 
 
+def assert_same_values(x, y, what):
+    """Bit for bit except NaN payloads and the sign of zeros (tests/test_gpu_horizon.py's
+    rule: the device drops the reference's exact-zero matrix terms, so an env
+    at rest right after an auto-reset may hold -0 where the oracle's +0 terms
+    give +0; nothing downstream tells them apart)."""
+    a = x.detach().cpu().numpy() if torch.is_tensor(x) else x
+    b = y.detach().cpu().numpy() if torch.is_tensor(y) else y
+    d = (a.view(np.int64) != b.view(np.int64)) & ~(np.isnan(a) & np.isnan(b)) & ~((a == 0) & (b == 0))
+    assert not d.any(), f"{what}: fields {[(int(f), int(d[f].sum())) for f in np.nonzero(d.any(1))[0]][:8]}"
+
+
 def _tiled(d, n):
     """n env states from the natural tumbling rows (the synthetic huge-angle
     ones are left out: their env-steps diverge), with step counters and
@@ -124,7 +135,7 @@ def _tiled(d, n):
     return s
 
 
-@pytest.mark.parametrize("rollout_kernel", [0, 1], ids=["k_rollout", "k_rollout_pair"])
+@pytest.mark.parametrize("rollout_kernel", [0, 1, 2], ids=["k_rollout", "k_rollout_pair", "k_rollout_split"])
 def test_tumbling_chained_equals_lockstep_oracle(tumble, rollout_kernel):
     """32 chained env-steps per env (salp_step_random(32): each env's steps
     back to back on the chained kernel) from tumbling states == 32 lock-step
@@ -139,14 +150,14 @@ def test_tumbling_chained_equals_lockstep_oracle(tumble, rollout_kernel):
     o = orc.Oracle(p, N_TILE, seed=5)
     o.state[:] = s0
     o.step_random(32, threads=_threads())
-    assert_bits_equal(env.get_state(), torch.tensor(o.state), "chained from tumbling states", nan_payloads=True)
+    assert_same_values(env.get_state(), o.state, "chained from tumbling states")
 
 
-@pytest.mark.parametrize("rollout_kernel", [0, 1], ids=["k_rollout", "k_rollout_pair"])
+@pytest.mark.parametrize("rollout_kernel", [0, 1, 2], ids=["k_rollout", "k_rollout_pair", "k_rollout_split"])
 def test_tumbling_rollout_is_split_invariant(tumble, rollout_kernel):
     """The chained rollout from tumbling states: one launch to 6 env-steps per
     env == the same work cut into 97-tick launches (state and steps_done bit
-    for bit, NaN payloads of diverging envs aside).  The headline's split test
+    for bit; a NaN's sign and payload aside, tests/test_gpu_headline.py).  The headline's split test
     starts from fresh resets, where the long roll / pitch path never runs."""
     s0 = _tiled(tumble, N_TILE)
     p = default_params()

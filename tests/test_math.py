@@ -171,9 +171,10 @@ def test_tick_yaw_sincos_large_angles():
 
 
 def test_tick_roll_pitch_pair():
-    """sm_sincos_rp2: the four-term kernels when neither |angle| exceeds 1/16
-    (or is NaN), within one ulp; the yaw's one-stage function for both
-    otherwise (round 5: branch-free; the tick_yaw test holds it to mpmath)."""
+    """sm_sincos_rp2 (round 6): the yaw's one-stage function for roll and
+    pitch at every size (rows 14-17 equal the yaw rows 12 / 13 of the same
+    angle bit for bit), within one ulp of mpmath on the small angles that most
+    ticks see; NaN in one angle leaves the other's sin / cos alone."""
     rng = np.random.default_rng(4)
     x = np.concatenate([rng.uniform(-0.0625, 0.0625, 4000), rng.uniform(-1e-6, 1e-6, 500), [0.0625, -0.0625, 0.0]])
     y = rng.uniform(-0.0625, 0.0625, len(x))
@@ -182,15 +183,13 @@ def test_tick_roll_pitch_pair():
         e, exact = _ulps(out[row], f, a)
         ok = np.abs(exact) > 1e-300
         assert np.max(e[ok]) <= 1.0, (row, float(np.max(e[ok])))
-    # one angle beyond 1/16: the yaw function for both (rows 12 / 13 are its sin / cos of x),
-    # tumbling angles of thousands of radians included
-    xb = np.concatenate([rng.uniform(-0.05, 0.05, 300), rng.uniform(0.07, 2.0, 300), rng.uniform(-5e3, 5e3, 300)])
-    yb = np.concatenate([rng.uniform(0.07, 2.0, 300), rng.uniform(-0.05, 0.05, 300), rng.uniform(-0.05, 0.05, 300)])
+    # every size, tumbling angles of thousands of radians included: the yaw function for both
+    xb = np.concatenate([x, rng.uniform(0.07, 2.0, 300), rng.uniform(-5e3, 5e3, 300)])
+    yb = np.concatenate([y, rng.uniform(-0.05, 0.05, 300), rng.uniform(-0.05, 0.05, 300)])
     ob = oracle.math_selftest(xb, yb)
     assert np.array_equal(ob[14], ob[12]) and np.array_equal(ob[15], ob[13])
     oy = oracle.math_selftest(yb, xb)
     assert np.array_equal(ob[16], oy[12]) and np.array_equal(ob[17], oy[13])
-    # NaN takes the short kernels (NaN out) and leaves the other angle on them too
     on = oracle.math_selftest(np.array([np.nan, 0.01]), np.array([0.01, np.nan]))
     ref = oracle.math_selftest(np.array([0.01]), np.array([0.0]))
     assert np.isnan(on[14][0]) and np.isnan(on[15][0]) and np.isnan(on[16][1]) and np.isnan(on[17][1])

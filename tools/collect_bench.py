@@ -1,5 +1,6 @@
 """salp_collect vs the plain chained rollout (same per-env step cap) vs
-lock-step salp_step, env-steps/s.  N="32768 65536" K=32 python tools/collect_bench.py"""
+lock-step salp_step, env-steps/s.  N="32768 65536" K=32 python tools/collect_bench.py
+(KERNEL = salp_set_rollout_kernel mode, default -1: the auto choice)"""
 import json
 import os
 import sys
@@ -25,6 +26,7 @@ def main():
     k = int(os.environ.get("K", 32))
     for n in [int(x) for x in os.environ.get("N", "32768 65536").split()]:
         env = BatchedSalpEnv(n, seed=0)
+        env.set_rollout_kernel(int(os.environ.get("KERNEL", "-1")))
         pol = ActorCritic(env.obs_dim, 3).cuda()
         w = pack_policy(pol)
         z = lambda *s: torch.zeros(s, dtype=torch.float32, device="cuda")  # noqa: E731
