@@ -677,6 +677,34 @@ SD bool next_tick_steady(const Hot& h, const Params& P) {
  * read the angles or the world position, so the kinematics only follow them
  * (k_step_wave runs them on a second wave).  SETTLED: see tick. */
 enum { TD_FORCES = 1, TD_KINEMATICS = 2, TD_POSITIONS = 4, TD_ALL = 7 };
+/* The angle chain of a tick (TD_KINEMATICS) on explicit values: the Euler
+ * angles, world position and roll / pitch sin / cos it carries, and this
+ * tick's integrated v and w (k_rollout_split's B wave runs it alone). */
+struct Kin { double e0, e1, e2, p0, p1, p2, sp, cp, st, cth; };
+SD void kinematics(Kin& k, double v0, double v1, double v2, double w0, double w1, double w2, const Params& P,
+                   double* rates) {
+    {   /* to_euler_angle_rate_jit (src/dynamics.py:20-31) at the current angles;
+         * product mode (the oracle's to_euler_angle_rate): u = sin(phi) w1 +
+         * cos(phi) w2, g = u / cos(theta) is row 2 and tan(theta) u = sin(theta) g
+         * row 0's tail */
+        const double u = sm_fma(k.cp, w2, k.sp * w1);
+        const double g2 = qdiv(u, rcp_of(k.cth));
+        const double r0 = sm_fma(k.st, g2, w0);
+        const double r1 = sm_fma(-k.sp, w2, k.cp * w1);
+        const double r2 = g2;
+        k.e0 = sm_mad(r0, DT, k.e0); k.e1 = sm_mad(r1, DT, k.e1); k.e2 = sm_mad(r2, DT, k.e2);
+        rates[0] = r0; rates[1] = r1; rates[2] = r2;
+    }
+    {   /* to_world_frame_jit (src/dynamics.py:34-58) at the new angles (world_frame;
+         * roll / pitch sin / cos kept for the next tick's Euler-rate map) */
+        double ss, cs;
+        sm_sincos_rp2(k.e0, k.e1, &k.sp, &k.cp, &k.st, &k.cth, P.sk);
+        sm_sincos_yaw_p(k.e2, &ss, &cs, P.sk);
+        double vw[3];
+        sm_world_frame(k.sp, k.cp, k.st, k.cth, ss, cs, v0, v1, v2, vw);
+        k.p0 = sm_mad(vw[0], DT, k.p0); k.p1 = sm_mad(vw[1], DT, k.p1); k.p2 = sm_mad(vw[2], DT, k.p2);
+    }
+}
 template <bool REC, bool RAND, bool SETTLED, int PARTS = TD_ALL>
 SD void tick_dynamics(Hot& h, const Params& P, double* rec, int64_t rs) {
     if (PARTS & TD_FORCES) {
@@ -813,30 +841,15 @@ SD void tick_dynamics(Hot& h, const Params& P, double* rec, int64_t rs) {
         h.w0 = sm_mad(nal0, DT, h.w0); h.w1 = sm_mad(nal1, DT, h.w1); h.w2 = sm_mad(nal2, DT, h.w2);
     }
     if (PARTS & TD_KINEMATICS) {
-        {   /* to_euler_angle_rate_jit (src/dynamics.py:20-31) at the current angles;
-             * product mode (the oracle's to_euler_angle_rate): u = sin(phi) w1 +
-             * cos(phi) w2, g = u / cos(theta) is row 2 and tan(theta) u = sin(theta) g
-             * row 0's tail */
-            const double u = sm_fma(h.cp, h.w2, h.sp * h.w1);
-            const double g2 = qdiv(u, rcp_of(h.cth));
-            double r0 = sm_fma(h.st, g2, h.w0);
-            double r1 = sm_fma(-h.sp, h.w2, h.cp * h.w1);
-            double r2 = g2;
-            h.e0 = sm_mad(r0, DT, h.e0); h.e1 = sm_mad(r1, DT, h.e1); h.e2 = sm_mad(r2, DT, h.e2);
-            if (REC) {
-                rec[(int64_t)SALP_T_ETAR0 * rs] = r0;
-                rec[(int64_t)SALP_T_ETAR1 * rs] = r1;
-                rec[(int64_t)SALP_T_ETAR2 * rs] = r2;
-            }
-        }
-        {   /* to_world_frame_jit (src/dynamics.py:34-58) at the new angles (world_frame;
-             * roll / pitch sin / cos kept for the next tick's Euler-rate map) */
-            double ss, cs;
-            sm_sincos_rp2(h.e0, h.e1, &h.sp, &h.cp, &h.st, &h.cth, P.sk);
-            sm_sincos_yaw_p(h.e2, &ss, &cs, P.sk);
-            double vw[3];
-            sm_world_frame(h.sp, h.cp, h.st, h.cth, ss, cs, h.v0, h.v1, h.v2, vw);
-            h.p0 = sm_mad(vw[0], DT, h.p0); h.p1 = sm_mad(vw[1], DT, h.p1); h.p2 = sm_mad(vw[2], DT, h.p2);
+        Kin k{h.e0, h.e1, h.e2, h.p0, h.p1, h.p2, h.sp, h.cp, h.st, h.cth};
+        double r[3];
+        kinematics(k, h.v0, h.v1, h.v2, h.w0, h.w1, h.w2, P, r);
+        h.e0 = k.e0; h.e1 = k.e1; h.e2 = k.e2; h.p0 = k.p0; h.p1 = k.p1; h.p2 = k.p2;
+        h.sp = k.sp; h.cp = k.cp; h.st = k.st; h.cth = k.cth;
+        if (REC) {
+            rec[(int64_t)SALP_T_ETAR0 * rs] = r[0];
+            rec[(int64_t)SALP_T_ETAR1 * rs] = r[1];
+            rec[(int64_t)SALP_T_ETAR2 * rs] = r[2];
         }
     }
     if (PARTS & TD_POSITIONS) {

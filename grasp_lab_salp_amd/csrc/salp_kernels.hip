@@ -14,6 +14,7 @@
 
 #include "salp_device.h"
 #include "salp_pair.h"
+#include "salp_tanh.h"
 
 using salp::Hot;
 using salp::Params;
@@ -367,23 +368,8 @@ typedef const __attribute__((address_space(4))) float* PolicyW;
 typedef float PolicyF2 __attribute__((ext_vector_type(2)));
 static_assert(kPH % 2 == 0, "hidden units go in pairs");
 
-// tanh of the policy's hidden units, branch-free: below |x| = 0.625 the odd
-// polynomial the device library uses there (x + x^3 P(x^2)), above it
-// 1 - 2 / (1 + 2^(2|x| log2 e)) on the hardware exp2 and reciprocal.  About
-// 1e-7 from torch's tanh (the library's tanhf is ~1 ulp, and runs both of its
-// paths in a wave with small and large units: 35 instructions against 17 here).
-// The collection tests hold values and log-probabilities to the torch policy.
-__device__ __forceinline__ float policy_tanh(float x) {
-    const float a = fabsf(x), z = x * x;
-    float p = fmaf(__builtin_bit_cast(float, 0xbbbac73du), z, __builtin_bit_cast(float, 0x3ca908c9u));
-    p = fmaf(z, p, __builtin_bit_cast(float, 0xbd5c1c4eu));
-    p = fmaf(z, p, __builtin_bit_cast(float, 0x3e088382u));
-    p = fmaf(z, p, __builtin_bit_cast(float, 0xbeaaaa99u));
-    const float small = fmaf(z, a * p, a);
-    const float e = __builtin_amdgcn_exp2f(a * 2.88539008177792681f);
-    const float large = fmaf(-2.0f, __builtin_amdgcn_rcpf(1.0f + e), 1.0f);
-    return copysignf(a < 0.625f ? small : large, x);
-}
+// tanh of the policy's hidden units: salp_tanh.h (shared with the PPO update).
+__device__ __forceinline__ float policy_tanh(float x) { return salp_tanhf(x); }
 
 __device__ __forceinline__ void policy_layer1(PolicyW w, int w1, int b1, const float* x, float* h1) {
 #pragma unroll
@@ -1687,9 +1673,16 @@ __device__ __forceinline__ void pair_wave_b(PairShared& sh, PairJobs* jobs, cons
         const salp::SpillSlot ns{sh.big + s, kPairEnvs};
         const salp::Cache32 c32{sh.cache32 + s, kPairEnvs};
         if constexpr (SPLIT) {
-            Hot h;
-            salp::unspill<false>(h, ns, P, 0);
-            if (!active) h.b2 = -INFINITY;
+            // the angle chain's state from the slot; the clock decides which
+            // wave-ticks this lane ticks, exactly as the A wave's copy does
+            const double sct = ns[salp::SP_CT];
+            double mx, b1, b2;
+            salp::cycle_bounds_of(ns[salp::SP_REFILL], ns[salp::SP_TURN], ns[salp::SP_JET], ns[salp::SP_COAST], &mx, &b1,
+                                  &b2);
+            if (!active) b2 = -INFINITY;
+            salp::Kin k{ns[salp::SP_E], ns[salp::SP_E + 1], ns[salp::SP_E + 2], ns[salp::SP_P], ns[salp::SP_P + 1],
+                        ns[salp::SP_P + 2], ns[salp::SP_SP], ns[salp::SP_CP], ns[salp::SP_ST], ns[salp::SP_CTH]};
+            double ct = sct;
             prof.lap(PP_BOUNDARY);
             __syncthreads();   // #2
             prof.lap(PP_BARRIER);
@@ -1700,7 +1693,8 @@ __device__ __forceinline__ void pair_wave_b(PairShared& sh, PairJobs* jobs, cons
                     // wait for wave-tick g, or the end of the chunk before it
                     int c = 0;
                     for (int it = 0;; ++it) {
-                        c = __hip_atomic_load(&sh.cnt[grp][0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        c = __builtin_amdgcn_readfirstlane(
+                            __hip_atomic_load(&sh.cnt[grp][0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
                         if ((c & ~kSplitEnd) > g || (c & kSplitEnd)) break;
                         if (it >= kPairSpin) {   /* give up: this chunk's results are invalid */
                             if (lane == 0) atomicAdd(&g_pair_timeouts, 1u);
@@ -1715,10 +1709,10 @@ __device__ __forceinline__ void pair_wave_b(PairShared& sh, PairJobs* jobs, cons
                     const double2 x0 = q[0], x1 = q[64], x2 = q[128];
                     pair_publish(&sh.cnt[grp][1], g + 1);   // slot read: the A wave may refill it
                     prof.lap(PP_READ);
-                    if (h.ct < h.b2) {
-                        h.v0 = x0.x; h.v1 = x0.y; h.v2 = x1.x; h.w0 = x1.y; h.w1 = x2.x; h.w2 = x2.y;
-                        salp::tick_dynamics<false, false, false, salp::TD_KINEMATICS>(h, PV, nullptr, 0);
-                        h.ct += salp::DT;
+                    if (ct < b2) {
+                        double r[3];
+                        salp::kinematics(k, x0.x, x0.y, x1.x, x1.y, x2.x, x2.y, PV, r);
+                        ct += salp::DT;
                     }
                     prof.lap(PP_TICK);
                 }
@@ -1727,9 +1721,9 @@ __device__ __forceinline__ void pair_wave_b(PairShared& sh, PairJobs* jobs, cons
             prof.lap(PP_BARRIER);
             __syncthreads();   // #3b: the A wave spilled its fields
             prof.lap(PP_BARRIER);
-            ns[salp::SP_E] = h.e0; ns[salp::SP_E + 1] = h.e1; ns[salp::SP_E + 2] = h.e2;
-            ns[salp::SP_P] = h.p0; ns[salp::SP_P + 1] = h.p1; ns[salp::SP_P + 2] = h.p2;
-            ns[salp::SP_SP] = h.sp; ns[salp::SP_CP] = h.cp; ns[salp::SP_ST] = h.st; ns[salp::SP_CTH] = h.cth;
+            ns[salp::SP_E] = k.e0; ns[salp::SP_E + 1] = k.e1; ns[salp::SP_E + 2] = k.e2;
+            ns[salp::SP_P] = k.p0; ns[salp::SP_P + 1] = k.p1; ns[salp::SP_P + 2] = k.p2;
+            ns[salp::SP_SP] = k.sp; ns[salp::SP_CP] = k.cp; ns[salp::SP_ST] = k.st; ns[salp::SP_CTH] = k.cth;
             prof.lap(PP_BOUNDARY);
             __syncthreads();   // #4
             prof.lap(PP_BARRIER);

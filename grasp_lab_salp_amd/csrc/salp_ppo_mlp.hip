@@ -24,7 +24,9 @@
 //                    clipping coefficient and Adam, in one block
 //
 // Between the last two a multi-GPU learner all-reduces the flat gradient
-// (one RCCL message).  Row math is float32 like torch's; reductions are fp64;
+// (one RCCL message).  The hidden units' tanh is the collection's
+// (salp_tanh.h: branch-free, ~1e-7 from torch's; the library's tanhf was 35
+// VALU instructions of the row kernel's ~115 per unit, profiles/r6c_pmc_update_summary.json).  Row math is float32 like torch's; reductions are fp64;
 // the results agree with torch to float32 rounding (tests/test_gpu_ppo_mlp.py),
 // not bit for bit (different summation orders), and are deterministic (no
 // atomics).
@@ -34,6 +36,7 @@
 #include <cstdint>
 
 #include "../../include/salp.h"
+#include "salp_tanh.h"
 
 namespace {
 
@@ -290,7 +293,7 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
                 acc = mfma32(sX[32 * qa + lc][k], sW1[net][32 * qb + lc][k], acc);
             }
 #pragma unroll
-            for (int r = 0; r < 16; ++r) sH1[net][32 * qa + crow(r, lh)][32 * qb + lc] = tanhf(acc[r]);
+            for (int r = 0; r < 16; ++r) sH1[net][32 * qa + crow(r, lh)][32 * qb + lc] = salp_tanhf(acc[r]);
         }
         __syncthreads();
         // ---- layer 2: h2 = tanh(h1 W2^T + b2)    (K = 64: 32 steps, k = 32 half + 4 s4 + e); h2 kept
@@ -309,7 +312,7 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                h2r[r] = tanhf(acc[r]);
+                h2r[r] = salp_tanhf(acc[r]);
                 sH2[net][32 * qa + crow(r, lh)][32 * qb + lc] = h2r[r];
             }
         }
