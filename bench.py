@@ -307,8 +307,8 @@ def ppo_leg(a, rank, world, dev):
 
 
 def collect_roofline(n, T, collect_s, parity):
-    """fp64 VALU roofline of the timed collection (the pair kernel
-    k_rollout_pair<true> at config 5's 32 768 envs): algorithmic flops
+    """fp64 VALU roofline of the timed collection (the two-wave kernel of the
+    auto choice at config 5's 32 768 envs, k_rollout_split<true> from round 6): algorithmic flops
     (F_TICK_ALGO per physics tick, the ticks measured by the collection's
     sampled replay) and, from a committed PMC summary of this config whose
     kernel fingerprint matches the library's, executed flops; both over the
@@ -320,13 +320,14 @@ def collect_roofline(n, T, collect_s, parity):
     if not collect_s:
         return None
     tps = parity["ticks_per_env_step"] if parity else None
-    res = {"bound": "fp64-valu", "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s", "kernel": "k_rollout_pair<true>",
+    symbol, kname = _codeobj.collect_kernel()
+    res = {"bound": "fp64-valu", "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s", "kernel": kname,
            "collect_s": collect_s, "ticks_per_env_step": tps}
     if tps:
         fl = F_TICK_ALGO * n * T * tps / collect_s / 1e12
         res.update({"achieved": fl, "frac": fl / FP64_VALU_PEAK_TFLOPS, "count": "algorithmic (F_TICK_ALGO x "
                     "measured ticks of the replayed env-steps)"})
-    sha = _codeobj.kernel_sha(LIB_PATH, _codeobj.PAIR_COLLECT_KERNEL)
+    sha = _codeobj.kernel_sha(LIB_PATH, symbol)
     res["kernel_sha16"] = sha
     best, stale = None, []
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_collect_summary.json")), key=summary_order):

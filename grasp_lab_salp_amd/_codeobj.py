@@ -124,5 +124,16 @@ def kernel_sha(lib_path, contains):
 
 # The bench's dominant kernel: k_rollout<RAND = false, POL = false>.
 ROLLOUT_KERNEL = "k_rolloutILb0ELb0EE"
-# The PPO leg's collection kernel (config 5, 32 768 envs): k_rollout_pair<POL = true>.
+# The PPO leg's collection kernel (config 5, 32 768 envs): the auto choice's
+# two-wave kernel with POL = true -- k_rollout_split<true> from round 6
+# (k_rollout_pair<true> with SALP_TWO_WAVE_KERNEL=pair).
 PAIR_COLLECT_KERNEL = "k_rollout_pairILb1EE"
+SPLIT_COLLECT_KERNEL = "k_rollout_splitILb1EE"
+
+
+def collect_kernel():
+    """(mangled-name fragment, display name) of the collection kernel the auto choice runs at config 5."""
+    import os
+    if (os.environ.get("SALP_TWO_WAVE_KERNEL") or "").startswith("p"):
+        return PAIR_COLLECT_KERNEL, "k_rollout_pair<true>"
+    return SPLIT_COLLECT_KERNEL, "k_rollout_split<true>"

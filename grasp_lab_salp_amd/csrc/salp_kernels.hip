@@ -2068,15 +2068,17 @@ bool use_pair(const SalpEnv* h) {
 }
 unsigned pair_blocks_for(int64_t n) { return (unsigned)((n + kPairEnvs - 1) / kPairEnvs); }
 // Of the two-wave kernels: the one-way split (k_rollout_split) in mode 2, the
-// Newton <-> Euler pair in mode 1; the auto choice's two-wave kernel is the
-// pair unless SALP_TWO_WAVE_KERNEL=split (A/B runs).
+// Newton <-> Euler pair in mode 1.  The auto choice's two-wave kernel is the
+// split (round 6: config 5's collection 27.2-27.9 vs 25.4-25.7 M env-steps/s,
+// PPO leg 20.3 vs 19.7 M on one box, profiles/r6_experiments.md r6d);
+// SALP_TWO_WAVE_KERNEL=pair selects the pair (A/B runs).
 bool use_split(const SalpEnv* h) {
     if (h->rollout_kernel >= 1) return h->rollout_kernel == 2;
-    static const bool split = [] {
+    static const bool pair = [] {
         const char* e = std::getenv("SALP_TWO_WAVE_KERNEL");
-        return e && e[0] == 's';
+        return e && e[0] == 'p';
     }();
-    return split;
+    return !pair;
 }
 // k_rollout_split's steady budgets (SALP_SPLIT_STEADY_Q8 / SALP_SPLIT_COLLECT_Q8
 // override them): its steady ticks lose the angle chain as its full ones do,

@@ -148,7 +148,7 @@ def test_pair_collect_equals_single_lane_collect(n, n_steps, max_cycles, kernel)
             assert _same(a[k], b[k]), k
 
 
-@pytest.mark.parametrize("kernel", [-1, 2], ids=["auto", "split"])
+@pytest.mark.parametrize("kernel", [-1, 1], ids=["auto", "pair"])
 def test_pair_collect_32768_envs_sampled_envs_replay_on_the_oracle(kernel):
     """The auto choice at 32 768 envs is a two-wave kernel.  256 sampled env ids
     (the first and last workgroup's seats included) are replayed on the C
