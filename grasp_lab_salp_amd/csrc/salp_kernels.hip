@@ -2082,7 +2082,10 @@ bool use_split(const SalpEnv* h) {
 }
 // k_rollout_split's steady budgets (SALP_SPLIT_STEADY_Q8 / SALP_SPLIT_COLLECT_Q8
 // override them): its steady ticks lose the angle chain as its full ones do,
-// so k_rollout's ratio is the starting point.
+// so k_rollout's ratio (560) is the rollout's; salp_collect's, swept on the
+// bench's PPO leg (chunk 128 / 144 / 176 / 208 / 256 x q 340 .. 1100,
+// profiles/r6_experiments.md r6g): q = 700 with the 176-tick chunk, PPO leg
+// 20.65 M (q 560: 20.30 M; q 900: 20.22 M).
 int32_t split_steady_q8() {
     static const int32_t q = [] {
         const char* e = std::getenv("SALP_SPLIT_STEADY_Q8");
@@ -2095,7 +2098,7 @@ int32_t split_collect_steady_q8() {
     static const int32_t q = [] {
         const char* e = std::getenv("SALP_SPLIT_COLLECT_Q8");
         const long v = e ? std::strtol(e, nullptr, 10) : 0;
-        return (int32_t)(v > 0 && v < (1 << 16) ? v : 560);
+        return (int32_t)(v > 0 && v < (1 << 16) ? v : 700);
     }();
     return q;
 }

@@ -1,5 +1,5 @@
 """salp_collect at BASELINE configs[4]'s size (32 768 envs, n_steps 256, the
-PPO leg's defaults: k_rollout_pair<true>, chunk 192) with a fresh 64-64 tanh
+PPO leg's defaults: the auto two-wave kernel, k_rollout_split<true> from round 6, chunk 176) with a fresh 64-64 tanh
 policy (seed 0), twice (the first dispatch is the warm-up the summary drops),
 for rocprofv3 --pmc passes (tools/gpu_pmc_collect.sh PROBE=1).  Prints the
 env-steps and the mean ticks per env-step of the second call's sampled replay

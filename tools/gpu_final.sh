@@ -4,7 +4,7 @@
 # the headline kernel and of config 5's collection kernel (through
 # tools/collect_pmc_probe.py), and the per-env step path's latency.  Then, here:
 #   python tools/pmc_summary.py TAG
-#   python tools/pmc_summary.py TAGc --kernel 'k_rollout_pair<true>' --symbol k_rollout_pairILb1EE \
+#   python tools/pmc_summary.py TAGc --kernel 'k_rollout_split<true>' --symbol k_rollout_splitILb1EE \
 #       --config-json '{"n_envs": 32768, "n_steps": 256}' --suffix pmc_collect_summary \
 #       --workload-json gpurun_out/TAG_collect_probe.json
 # TAG names the outputs under gpurun_out/ (the collection's PMC passes: TAGc).

@@ -1,8 +1,8 @@
 #!/bin/bash
 # PMC passes over the bench's PPO leg (config 5: salp_collect on
-# k_rollout_pair<true> at 32 768 envs, n_steps 256), one counter group per
+# the auto two-wave kernel, k_rollout_split<true> from round 6, at 32 768 envs, n_steps 256), one counter group per
 # pass, kernel trace only; summarise with
-#   python tools/pmc_summary.py TAG --kernel 'k_rollout_pair<true>' --symbol k_rollout_pairILb1EE \
+#   python tools/pmc_summary.py TAG --kernel 'k_rollout_split<true>' --symbol k_rollout_splitILb1EE \
 #       --config-json '{"n_envs": 32768, "n_steps": 256}' --suffix pmc_collect_summary
 # (the PPO leg runs two collections: warm-up and timed; the summary keeps the timed one).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
