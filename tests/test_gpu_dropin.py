@@ -193,6 +193,65 @@ def test_salp_robot_env_reproduces_reference_episodes(job):
     env.close()
 
 
+DROPIN_SCRIPT = """
+import json, sys
+import numpy as np
+from robot import Robot, Nozzle
+from salp_robot_env import SalpRobotEnv
+
+def make_env():
+    nozzle = Nozzle(length1=0.05, length2=0.05, length3=0.05, area=0.00016, mass=1.0)
+    robot = Robot(dry_mass=1.0, init_length=0.3, init_width=0.15, max_contraction=0.06, nozzle=nozzle)
+    robot.nozzle.set_angles(angle1=0.0, angle2=0.0)
+    robot.set_environment(density=1000)
+    return SalpRobotEnv(render_mode=None, robot=robot)
+
+if __name__ == "__main__":
+    actions = np.load(sys.argv[1])
+    np.random.seed(int(sys.argv[2]))
+    env = make_env()
+    env.reset()
+    out = []
+    for a in actions:
+        obs, rew, term, trunc, info = env.step(a)
+        out.append([obs.tolist(), float(rew), bool(term), bool(trunc)])
+    print("RESULT " + json.dumps({"module": SalpRobotEnv.__module__, "steps": out}))
+"""
+
+
+def test_dropin_launcher_runs_a_reference_episode(tmp_path):
+    """``python -m grasp_lab_salp_amd.dropin`` on a script written exactly as
+    src/train_robot.py's make_env (reference imports, a decoy ``robot.py`` beside
+    it) reproduces fixture episode 1 (same tolerances as above)."""
+    import os
+    import subprocess
+    import sys
+
+    d = load_episodes()
+    rows = np.where(d["job_index"] == 1)[0]
+    assert int(d["num_obstacles_cfg"][rows[0]]) == 2
+    np.save(tmp_path / "actions.npy", np.asarray(d["action"][rows], np.float32))
+    (tmp_path / "robot.py").write_text("raise ImportError('reference robot.py imported')\n")
+    (tmp_path / "train_robot.py").write_text(DROPIN_SCRIPT)
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=repo + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    out = subprocess.run([sys.executable, "-m", "grasp_lab_salp_amd.dropin", str(tmp_path / "train_robot.py"),
+                          str(tmp_path / "actions.npy"), "1"], cwd=str(tmp_path), env=env,
+                         capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [l for l in out.stdout.splitlines() if l.startswith("RESULT ")][-1]
+    res = __import__("json").loads(line[len("RESULT "):])
+    assert res["module"] == "grasp_lab_salp_amd.salp_robot_env"
+    for r, (obs, rew, term, trunc) in zip(rows, res["steps"]):
+        ref = d["obs"][r][:10]
+        obs = np.asarray(obs, np.float32)
+        assert np.max(np.abs(obs - ref) / np.maximum(np.abs(ref), 1e-3)) <= 1e-5, r
+        assert abs(rew - d["reward"][r]) <= 1e-4
+        assert (term, trunc) == (bool(d["terminated"][r]), bool(d["truncated"][r]))
+        if term or trunc:
+            break
+
+
 def test_salp_robot_env_robot_views_and_recording():
     env = _make_env()
     env.robot.enable_history_recording()
