@@ -34,8 +34,13 @@ def main():
         return m.group(0) + f" {{ const uint64_t t_ = clock64(); prof_[{i}] += t_ - tmark_; tmark_ = t_; }}"
     body = re.sub(r"__syncthreads\(\);", mark, body)
     assert n[0] < NPH, n[0]
-    body = (f"\n    uint64_t prof_[{NPH}] = {{}};\n    uint64_t tmark_ = clock64();" + body +
+    # the last two slots: the wave's start and end on the constant 100 MHz clock
+    # (wall_clock64, one clock for the whole device): the launch skew and each wave's span
+    assert n[0] + 1 < NPH - 2, n[0]
+    body = (f"\n    uint64_t prof_[{NPH}] = {{}};\n    prof_[{NPH - 2}] = wall_clock64();\n"
+            f"    uint64_t tmark_ = clock64();" + body +
             f"\n    {{ const uint64_t t_ = clock64(); prof_[{n[0]}] += t_ - tmark_; }}\n"
+            f"    prof_[{NPH - 1}] = wall_clock64();\n"
             f"    if ((threadIdx.x & 63) == 0)\n        for (int q = 0; q < {NPH}; ++q) "
             f"g_mlp_dbg[((size_t)blockIdx.x * (NT / 64) + threadIdx.x / 64) * {NPH} + q] = prof_[q];")
     s = s[:a] + body + s[b:]

@@ -32,10 +32,19 @@ def main():
     n = 256 * 8
     a = np.zeros((n, NPH), dtype=np.uint64)
     assert L.salp_debug_mlp_prof(a.ctypes.data, n) == 0
-    w = a.astype(np.float64)
+    w = a[:, :NPH - 2].astype(np.float64)
     tot = w.sum(1)
+    t0, t1 = a[:, NPH - 2].astype(np.int64), a[:, NPH - 1].astype(np.int64)
+    base = t0.min()
     print(json.dumps({"frac_by_barrier": [round(float(x), 4) for x in w.sum(0) / tot.sum()],
-                      "wave_cycles_mean": float(tot.mean())}))
+                      "cycles_by_barrier_mean": [round(float(x)) for x in w.mean(0)],
+                      "wave_cycles_mean": float(tot.mean()),
+                      # wall_clock64: 100 MHz
+                      "wave_start_us": {"p50": float(np.percentile(t0 - base, 50)) / 100,
+                                        "max": float((t0 - base).max()) / 100},
+                      "wave_end_us": {"p50": float(np.percentile(t1 - base, 50)) / 100,
+                                      "max": float((t1 - base).max()) / 100},
+                      "wave_span_us_mean": float((t1 - t0).mean()) / 100}))
 
 
 if __name__ == "__main__":
