@@ -6,7 +6,7 @@ drift apart silently.
 """
 import ctypes
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 # rows of salp_math_selftest's output (include/salp.h)
 MATH_SELFTEST_ROWS = 23
 MAX_OBSTACLES = 4

@@ -78,16 +78,18 @@ class SalpPpoMinibatch(ctypes.Structure):
         ("workspace", ctypes.c_void_p),
         ("stats", ctypes.c_void_p),
         ("adv_part", ctypes.c_void_p),
+        ("norm_part", ctypes.c_void_p),
     ]
 
 
 ADV_PARTIAL_DOUBLES = 512   # include/salp.h SALP_PPO_ADV_PARTIAL_DOUBLES
+APPLY_WORKSPACE_DOUBLES = 256   # include/salp.h SALP_PPO_APPLY_WORKSPACE_DOUBLES
 
 
 class SalpPpoAdam(ctypes.Structure):
     _fields_ = [
         ("obs_dim", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("norm_ready", ctypes.c_int32),
         ("params", ctypes.c_void_p * N_MLP_TENSORS),
         ("grads", ctypes.c_void_p),
         ("exp_avg", ctypes.c_void_p),
@@ -99,6 +101,7 @@ class SalpPpoAdam(ctypes.Structure):
         ("beta2", ctypes.c_double),
         ("eps", ctypes.c_double),
         ("max_grad_norm", ctypes.c_double),
+        ("workspace", ctypes.c_void_p),
     ]
 
 

@@ -8,7 +8,7 @@
 // ops: forward of both networks, the clipped-surrogate / value / entropy loss
 // (salp_ppo.hip's head), backward, clip_grad_norm_(max_norm) and Adam.  In
 // torch that is ~60 small kernels per minibatch (GEMMs, elementwise, reduce,
-// foreach); here it is four launches:
+// foreach); here it is four launches on one rank:
 //
 //   k_mlp_adv_sums   block partials of sum(adv), sum(adv^2) over the gathered
 //                    rows (the advantage normalisation's mean / std)
@@ -19,17 +19,20 @@
 //                    gradients, which the block accumulates in registers over
 //                    its tiles and writes as one fp32 partial per parameter
 //   k_mlp_reduce     sums the partials in fp64 into the flat gradient, and
-//                    the loss statistics
-//   k_mlp_apply      (salp_ppo_mlp_apply) the global gradient norm, the
-//                    clipping coefficient and Adam, in one block
+//                    the loss statistics (and, on one rank, the squared
+//                    norm's partials)
+//   k_mlp_adam       (salp_ppo_mlp_apply) the global gradient norm, the
+//                    clipping coefficient and Adam, one parameter per thread
+//                    (after k_mlp_norm's norm partials on several ranks; with
+//                    no workspace, k_mlp_apply does it all in one block)
 //
-// Between the last two a multi-GPU learner all-reduces the flat gradient
-// (one RCCL message).  The hidden units' tanh is the collection's
+// Between the reduction and the update a multi-GPU learner all-reduces the
+// flat gradient (one RCCL message).  The hidden units' tanh is the collection's
 // (salp_tanh.h: branch-free, ~1e-7 from torch's; the library's tanhf was 35
 // VALU instructions of the row kernel's ~115 per unit, profiles/r6c_pmc_update_summary.json).  Row math is float32 like torch's; reductions are fp64;
 // the results agree with torch to float32 rounding (tests/test_gpu_ppo_mlp.py),
 // not bit for bit (different summation orders), and are deterministic (no
-// atomics).
+// floating-point atomics: k_mlp_adam's one atomic counts arriving blocks).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -116,6 +119,28 @@ __device__ __forceinline__ void block_sums(double (&v)[K], double* sh, int nthre
     }
 }
 
+// The same sums in the same order, valid in thread 0 only (no broadcast: the
+// other threads skip the K x waves LDS reads).
+template <int K>
+__device__ __forceinline__ void block_sums0(double (&v)[K], double* sh, int nthreads) {
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k] += __shfl_xor(v[k], o, 64);
+    const int w = threadIdx.x / 64, l = threadIdx.x % 64;
+    __syncthreads();
+    if (l == 0)
+#pragma unroll
+        for (int k = 0; k < K; ++k) sh[w * K + k] = v[k];
+    __syncthreads();
+    if (threadIdx.x == 0)
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            double t = 0.0;
+            for (int ww = 0; ww < nthreads / 64; ++ww) t += sh[ww * K + k];
+            v[k] = t;
+        }
+}
+
 // blockIdx.y: minibatch (rows idx[y * B ...]), part + y * 2 * NADV (one launch
 // per epoch, salp_ppo_mlp_adv_partials; gridDim.y = 1 for one minibatch).
 __global__ __launch_bounds__(256) void k_mlp_adv_sums(int64_t B, const int64_t* __restrict__ idx,
@@ -162,6 +187,30 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
     const int D = m.obs_dim;
     const int64_t B = m.batch;
     const int tid = threadIdx.x;
+    const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_block;
+    const int64_t r_end = r_begin + a.rows_per_block < B ? r_begin + a.rows_per_block : B;
+    static_assert(TR * DP == 2 * NT, "two observation entries per thread and tile");
+    // observations of a tile (gathered rows; padding rows are zero), loaded a
+    // tile ahead into registers: entries tid and tid + NT of the [TR][DP] tile
+    auto load_x = [&](int64_t row0, float* xv) {
+        const int64_t n = r_end - row0;
+        for (int u = 0; u < 2; ++u) {
+            const int e = tid + u * NT, r = e / DP, k = e % DP;
+            xv[u] = (r < n && k < D) ? m.obs[m.idx[row0 + r] * D + k] : 0.0f;
+        }
+    };
+    float xv[2];
+    // the first tile's gather (index, then row: two dependent round trips) is
+    // issued before the weight staging, so the two latencies overlap
+    if (r_begin < r_end) load_x(r_begin, xv);
+    // and so are the advantage partials (summed after it)
+    static_assert(NADV <= NT, "one advantage partial per thread");
+    const bool norm_adv = m.normalize_advantage && B > 1;
+    double sq[2] = {0.0, 0.0};
+    if (norm_adv && tid < NADV) {
+        sq[0] = a.adv_part[2 * tid];
+        sq[1] = a.adv_part[2 * tid + 1];
+    }
     // weights (nets: 0 = actor / pi, 1 = critic / vf)
     __shared__ float sW1[2][H][DP];       // [net][unit][input]
     __shared__ float sB1[2][H];
@@ -216,10 +265,8 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
     }
     if (tid == 0) sVb = m.params[SALP_MLP_VAL_B][0];
     // advantage mean / std of the minibatch from k_mlp_adv_sums' partials, summed by the block
-    if (m.normalize_advantage && B > 1) {
-        static_assert(NADV <= NT, "one advantage partial per thread");
-        double sq[2] = {tid < NADV ? a.adv_part[2 * tid] : 0.0, tid < NADV ? a.adv_part[2 * tid + 1] : 0.0};
-        block_sums(sq, sRed, NT);
+    if (norm_adv) {
+        block_sums0(sq, sRed, NT);
         if (tid == 0) {
             const double mu = sq[0] / (double)B;
             const double var = fmax(sq[1] - sq[0] * mu, 0.0) / (double)(B - 1);
@@ -253,20 +300,6 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
     const float vw = sVw[32 * qb + lc];
     const float invB = 1.0f / (float)B, clip = (float)m.clip_range, vfc = (float)m.vf_coef;
     const float amean = sNorm[0], ainv = sNorm[1];
-    const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_block;
-    const int64_t r_end = r_begin + a.rows_per_block < B ? r_begin + a.rows_per_block : B;
-    static_assert(TR * DP == 2 * NT, "two observation entries per thread and tile");
-    // observations of a tile (gathered rows; padding rows are zero), loaded a
-    // tile ahead into registers: entries tid and tid + NT of the [TR][DP] tile
-    auto load_x = [&](int64_t row0, float* xv) {
-        const int64_t n = r_end - row0;
-        for (int u = 0; u < 2; ++u) {
-            const int e = tid + u * NT, r = e / DP, k = e % DP;
-            xv[u] = (r < n && k < D) ? m.obs[m.idx[row0 + r] * D + k] : 0.0f;
-        }
-    };
-    float xv[2];
-    if (r_begin < r_end) load_x(r_begin, xv);
 
     for (int64_t row0 = r_begin; row0 < r_end; row0 += TR) {
         const int nrows = (int)(r_end - row0 < TR ? r_end - row0 : TR);
@@ -473,7 +506,7 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
     for (int c = 0; c <= NA; ++c) red[c] = gHb[c];
 #pragma unroll
     for (int k = 0; k < NSTAT; ++k) red[NA + 1 + k] = st[k];
-    block_sums(red, sRed, NT);
+    block_sums0(red, sRed, NT);
     if (tid == 0) {
         for (int c = 0; c <= NA; ++c) P[c < NA ? a.L.off[SALP_MLP_ACT_B] + c : a.L.off[SALP_MLP_VAL_B]] = (float)red[c];
         for (int k = 0; k < NSTAT; ++k) a.stat_part[(int64_t)blockIdx.x * NSTAT + k] = red[NA + 1 + k];
@@ -508,12 +541,20 @@ __global__ __launch_bounds__(NT_RED) void k_mlp_reduce(SalpPpoMinibatch m, Layou
     }
     sh[g][l] = s;
     __syncthreads();
+    float gf = 0.0f;
     if (g == 0 && p < P) {
         double t = 0.0;
 #pragma unroll
         for (int k = 0; k < RED_G; ++k) t += sh[k][l];
         if (is_ls) t = (double)((float)t - (float)m.ent_coef);
-        m.grads[p] = (float)t;
+        gf = (float)t;
+        m.grads[p] = gf;
+    }
+    if (g == 0 && m.norm_part) {
+        // this block's 64 parameters' share of the squared norm, in k_mlp_norm's order
+        double q = (double)gf * (double)gf;
+        for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+        if (l == 0) m.norm_part[blockIdx.x] = q;
     }
     if (blockIdx.x == 0 && g == 1 && m.stats) {
         // every lane's partials loaded at once, then summed in the same order
@@ -626,6 +667,100 @@ __global__ __launch_bounds__(NT_APPLY) void k_mlp_apply(SalpPpoAdam o, Layout L)
     if (threadIdx.x == 0) o.step[0] = step;
 }
 
+// The same clip + Adam over many blocks (SalpPpoAdam.workspace set, ABI 13).
+// The squared norm's partials, one per 64 parameters (a wave's xor tree over
+// (double) g^2), come from k_mlp_reduce (SalpPpoMinibatch.norm_part: one rank)
+// or from k_mlp_norm (after a multi-GPU all-reduce); the two give the same
+// bits.  k_mlp_adam runs one parameter per thread; every block sums the
+// partials in the same fixed order, so every block derives the same norm and
+// clipping coefficient (deterministic), and the last block to arrive (a
+// vector atomic count in the workspace, after every block has read the step)
+// writes Adam's new step count.  r6m: the one-block kernel above took 10.6 us
+// per minibatch (~60 instructions per parameter on one CU); r5v's many-block
+// variant had re-read the whole gradient in every block for the norm.
+constexpr int NT_ADAM = 256;
+constexpr int NORM_PARTS_MAX = SALP_PPO_APPLY_WORKSPACE_DOUBLES - 1;   // the last slot: the arrival count
+constexpr int NORM_LANE_PARTS = (NORM_PARTS_MAX + 63) / 64;
+static_assert((2 * (H * DP + H + H * H + H) + NA * H + 2 * NA + H + 1 + 63) / 64 <= NORM_PARTS_MAX,
+              "the norm partials of obs_dim <= 16 fit the workspace");
+__global__ __launch_bounds__(NT_ADAM) void k_mlp_norm(SalpPpoAdam o, int P) {
+    const int p = blockIdx.x * NT_ADAM + threadIdx.x;
+    double q = 0.0;
+    if (p < P) {
+        const float g = o.grads[p];
+        q = (double)g * (double)g;
+    }
+    for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off, 64);
+    if (threadIdx.x % 64 == 0 && p < P) o.workspace[p / 64] = q;
+}
+
+__global__ __launch_bounds__(NT_ADAM) void k_mlp_adam(SalpPpoAdam o, Layout L) {
+    __shared__ float* s_base[SALP_MLP_N_TENSORS];   // params[t] - off[t]: p indexes it directly
+    __shared__ int s_off[SALP_MLP_N_TENSORS];
+    __shared__ float s_k[3];                        // clipping coefficient, lr / (1 - beta1^step), sqrt(1 - beta2^step)
+#pragma unroll
+    for (int t = 0; t < SALP_MLP_N_TENSORS; ++t)
+        if (threadIdx.x == t) {
+            s_base[t] = o.params[t] - L.off[t];
+            s_off[t] = (int)L.off[t];
+        }
+    const int P = (int)L.off[SALP_MLP_N_TENSORS];
+    const int nparts = (P + 63) / 64;
+    const int p = blockIdx.x * NT_ADAM + threadIdx.x;
+    float g = 0.0f, m1 = 0.0f, v1 = 0.0f;
+    if (p < P) {
+        g = o.grads[p];
+        m1 = o.exp_avg[p];
+        v1 = o.exp_avg_sq[p];
+    }
+    const float b1 = (float)o.beta1, b2 = (float)o.beta2, lr = (float)o.lr, eps = (float)o.eps;
+    if (threadIdx.x < 64) {
+        // the norm: lane l adds partials l, l + 64, ... in order, then the xor tree
+        double q = 0.0;
+#pragma unroll
+        for (int j = 0; j < NORM_LANE_PARTS; ++j) {
+            const int k = threadIdx.x + 64 * j;
+            q += k < nparts ? o.workspace[k] : 0.0;
+        }
+        for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off, 64);
+        const float step = o.step[0] + 1.0f;
+        const float bc1 = 1.0f - powf(b1, step), bc2 = 1.0f - powf(b2, step);
+        if (threadIdx.x == 0) {
+            const float total = (float)sqrt(q);
+            float coef = 1.0f;
+            if (o.max_grad_norm > 0.0) {
+                coef = (float)o.max_grad_norm / (total + 1e-6f);
+                coef = coef < 1.0f ? coef : 1.0f;
+            }
+            s_k[0] = coef;
+            s_k[1] = lr / bc1;
+            s_k[2] = sqrtf(bc2);
+            if (blockIdx.x == 0 && o.grad_norm) o.grad_norm[0] = total;
+            // every block has read the step count before it arrives; the last one advances it
+            unsigned* const arrived = reinterpret_cast<unsigned*>(o.workspace + NORM_PARTS_MAX);
+            if (atomicAdd(arrived, 1u) == gridDim.x - 1) {
+                o.step[0] = step;
+                *arrived = 0u;
+            }
+        }
+    }
+    __syncthreads();
+    if (p < P) {
+        int t = 0;
+#pragma unroll
+        for (int u = 1; u < SALP_MLP_N_TENSORS; ++u) t += p >= s_off[u] ? 1 : 0;
+        float* const wp = s_base[t] + p;
+        const float w1 = *wp;
+        const float coef = s_k[0], step_size = s_k[1], bc2_sqrt = s_k[2];
+        const float gc = g * coef;
+        const float m = b1 * m1 + (1.0f - b1) * gc;
+        const float v = b2 * v1 + (1.0f - b2) * gc * gc;
+        o.exp_avg[p] = m;
+        o.exp_avg_sq[p] = v;
+        *wp = w1 - step_size * m / (sqrtf(v) / bc2_sqrt + eps);
+    }
+}
+
 }  // namespace
 
 extern "C" __attribute__((visibility("hidden"))) int64_t salp_ppo_mlp_params_impl(int obs_dim) {
@@ -680,6 +815,13 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t salp_ppo_mlp_adv_par
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t salp_ppo_mlp_apply_launch(const SalpPpoAdam* o,
                                                                                        void* stream) {
-    hipLaunchKernelGGL(k_mlp_apply, dim3(1), dim3(NT_APPLY), 0, (hipStream_t)stream, *o, make_layout(o->obs_dim));
+    const Layout L = make_layout(o->obs_dim);
+    if (o->workspace) {
+        const int P = (int)L.off[SALP_MLP_N_TENSORS], nb = (P + NT_ADAM - 1) / NT_ADAM;
+        if (!o->norm_ready) hipLaunchKernelGGL(k_mlp_norm, dim3(nb), dim3(NT_ADAM), 0, (hipStream_t)stream, *o, P);
+        hipLaunchKernelGGL(k_mlp_adam, dim3(nb), dim3(NT_ADAM), 0, (hipStream_t)stream, *o, L);
+    } else {
+        hipLaunchKernelGGL(k_mlp_apply, dim3(1), dim3(NT_APPLY), 0, (hipStream_t)stream, *o, L);
+    }
     return hipGetLastError();
 }

@@ -482,6 +482,16 @@ class PPO:
                                         max_grad_norm=float(self.max_grad_norm if self.max_grad_norm else 0.0))
         for i, t in enumerate(self._mlp_tensors):
             self._f_adam.params[i] = t.data_ptr()
+        # clip + Adam over many blocks (k_mlp_adam, ABI 13), the squared norm's partials written by the
+        # gradient reduction itself on one rank (after the all-reduce, by k_mlp_norm, on several);
+        # SALP_PPO_APPLY=one keeps the one-block kernel (k_mlp_apply), for A / B runs
+        self._f_apply_ws = torch.zeros(_lib.APPLY_WORKSPACE_DOUBLES, dtype=torch.float64, device=self.device)
+        self._f_norm_part = None
+        if os.environ.get("SALP_PPO_APPLY", "blocks") != "one":
+            self._f_adam.workspace = self._f_apply_ws.data_ptr()
+            if not self._multi:
+                self._f_adam.norm_ready = 1
+                self._f_norm_part = self._f_apply_ws.data_ptr()
 
     def _fused_minibatch(self, idx, acc, part="all", adv_part=None):
         """One SB3 PPO minibatch step through salp_ppo_mlp: gradient of the
@@ -504,7 +514,8 @@ class PPO:
                                   returns=b.returns.data_ptr(), grads=self._f_grads.data_ptr(),
                                   clip_range=self._clip(), ent_coef=float(self.ent_coef), vf_coef=float(self.vf_coef),
                                   workspace=self._f_ws.data_ptr(), stats=acc.data_ptr(),
-                                  adv_part=adv_part.data_ptr() if adv_part is not None else None)
+                                  adv_part=adv_part.data_ptr() if adv_part is not None else None,
+                                  norm_part=self._f_norm_part)
         for i, t in enumerate(self._mlp_tensors):
             m.params[i] = t.data_ptr()
         _lib.check(L.salp_ppo_mlp_grads(ctypes.byref(m), stream))

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define SALP_ABI_VERSION 12
+#define SALP_ABI_VERSION 13
 
 #define SALP_MAX_OBSTACLES 4
 #define SALP_OBS_DIM_MAX (6 + 2 * SALP_MAX_OBSTACLES)
@@ -338,6 +338,10 @@ typedef struct SalpPpoMinibatch {
     float* stats;          /* [4] accumulated, or NULL */
     const double* adv_part; /* ABI 12: this minibatch's advantage partials from
                                salp_ppo_mlp_adv_partials, or NULL (computed here) */
+    double* norm_part;     /* ABI 13: or NULL.  The squared norm's partials of the final gradient (one per
+                              64 parameters), written by the reduction: pass SalpPpoAdam.workspace here and
+                              set SalpPpoAdam.norm_ready when nothing changes grads between the two calls
+                              (one rank; a multi-GPU learner's all-reduce does) */
 } SalpPpoMinibatch;
 int salp_ppo_mlp_grads(const SalpPpoMinibatch* m, void* stream);
 /* The advantage normalisation's partial sums (sum, sum of squares in fp64;
@@ -357,7 +361,8 @@ int salp_ppo_mlp_adv_partials(int64_t batch, int64_t n_minibatches, const int64_
  * multi-GPU learner all-reduces grads between the two calls. */
 typedef struct SalpPpoAdam {
     int32_t obs_dim;
-    int32_t reserved;
+    int32_t norm_ready;    /* ABI 13: 1 = workspace already holds the norm partials of grads
+                              (SalpPpoMinibatch.norm_part); 0 = computed here (k_mlp_norm) */
     float* params[SALP_MLP_N_TENSORS];
     const float* grads;
     float* exp_avg;
@@ -369,7 +374,12 @@ typedef struct SalpPpoAdam {
     double beta2;
     double eps;
     double max_grad_norm;
+    double* workspace;     /* ABI 13: SALP_PPO_APPLY_WORKSPACE_DOUBLES, zero-filled once by the caller and
+                              then left to these calls (the norm's partials and a block-arrival count):
+                              clip + Adam run over many blocks (k_mlp_adam, after k_mlp_norm unless
+                              norm_ready); NULL: one block does both (k_mlp_apply) */
 } SalpPpoAdam;
+#define SALP_PPO_APPLY_WORKSPACE_DOUBLES 256
 int salp_ppo_mlp_apply(const SalpPpoAdam* a, void* stream);
 
 /* The LSTM cell of RecurrentPPO's MlpLstmPolicy (sb3-contrib RecurrentPPO,

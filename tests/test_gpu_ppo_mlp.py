@@ -172,3 +172,67 @@ def test_fused_graph_is_kept_and_equals_eager(max_mb):
     assert all(bool(torch.isfinite(t).all()) for t in sg)
     for pg, vf in hg:
         assert np.isfinite(vf) and np.isfinite(pg)
+
+
+@pytest.mark.parametrize("max_norm", [0.5, 1e9, 0.0])
+def test_apply_many_blocks_equals_one_block(max_norm):
+    """salp_ppo_mlp_apply with a workspace (ABI 13: k_mlp_norm + k_mlp_adam, one
+    parameter per thread) against the one-block kernel (workspace NULL) from the
+    same state, three steps with clipping active, inactive and off: the same
+    Adam arithmetic per parameter; only the squared norm's fp64 summation order
+    differs, so the norm agrees to float32 rounding and the parameters, moments
+    and step count to within one rounding of the clipping coefficient.  Then
+    the one-rank path: the gradient reduction's own norm partials
+    (SalpPpoMinibatch.norm_part, norm_ready) equal k_mlp_norm's bit for bit."""
+    import ctypes
+    from grasp_lab_salp_amd import _lib
+    L = _lib.load()
+    a = _model(True, max_grad_norm=max_norm)
+    g = torch.Generator(device="cuda").manual_seed(7)
+    state = [t.detach() for t in a._mlp_tensors] + [a._f_m, a._f_v, a._f_step]
+    snap = [t.clone() for t in state]
+    res = []
+    for ws in (None, a._f_apply_ws.data_ptr()):
+        with torch.no_grad():
+            for t, s in zip(state, snap):
+                t.copy_(s)
+        a._f_adam.workspace = ws
+        a._f_adam.norm_ready = 0   # grads are written below: k_mlp_norm recomputes the partials
+        g.manual_seed(7)
+        norms = []
+        for _ in range(3):
+            a._f_grads.copy_(torch.randn(a._f_grads.shape, generator=g, device="cuda") * 0.05)
+            _lib.check(L.salp_ppo_mlp_apply(ctypes.byref(a._f_adam), None))
+            torch.cuda.synchronize()
+            norms.append(float(a._f_gnorm))
+        res.append(([t.clone() for t in state], norms))
+    (s1, n1), (s2, n2) = res
+    assert float(s1[-1]) == float(s2[-1]) == float(snap[-1]) + 3
+    for x, y in zip(n1, n2):
+        assert abs(x - y) <= 2e-7 * abs(x), (n1, n2)
+    for x, y in zip(s1[:-1], s2[:-1]):
+        assert float((x - y).abs().max()) <= 1e-6 * max(1.0, float(y.abs().max())), float((x - y).abs().max())
+    # the reduction's partials (one rank) against k_mlp_norm's, on a real gradient
+    b = a.buf
+    _fill(a)
+    idx = torch.randperm(N_ENVS * N_STEPS, device="cuda")[:4096]
+    m = _lib.SalpPpoMinibatch(batch=idx.numel(), obs_dim=a.obs_dim, normalize_advantage=1, idx=idx.data_ptr(),
+                              obs=b.obs.data_ptr(), actions=b.actions.data_ptr(),
+                              old_log_prob=b.log_probs.data_ptr(), advantages=b.advantages.data_ptr(),
+                              returns=b.returns.data_ptr(), grads=a._f_grads.data_ptr(), clip_range=0.2,
+                              ent_coef=0.01, vf_coef=0.5, workspace=a._f_ws.data_ptr(),
+                              norm_part=a._f_apply_ws.data_ptr())
+    for i, t in enumerate(a._mlp_tensors):
+        m.params[i] = t.data_ptr()
+    a._f_apply_ws.zero_()
+    _lib.check(L.salp_ppo_mlp_grads(ctypes.byref(m), None))
+    torch.cuda.synchronize()
+    from_reduce = a._f_apply_ws.clone()
+    a._f_apply_ws.zero_()
+    a._f_adam.norm_ready = 0
+    a._f_adam.workspace = a._f_apply_ws.data_ptr()
+    _lib.check(L.salp_ppo_mlp_apply(ctypes.byref(a._f_adam), None))
+    torch.cuda.synchronize()
+    nparts = (a._f_grads.numel() + 63) // 64
+    assert torch.equal(from_reduce[:nparts], a._f_apply_ws[:nparts])
+    assert float(from_reduce[:nparts].sum()) > 0
