@@ -190,19 +190,46 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
     const int64_t r_begin = (int64_t)blockIdx.x * a.rows_per_block;
     const int64_t r_end = r_begin + a.rows_per_block < B ? r_begin + a.rows_per_block : B;
     static_assert(TR * DP == 2 * NT, "two observation entries per thread and tile");
-    // observations of a tile (gathered rows; padding rows are zero), loaded a
-    // tile ahead into registers: entries tid and tid + NT of the [TR][DP] tile
-    auto load_x = [&](int64_t row0, float* xv) {
+    // The gathered rows come in two dependent round trips (the index, then the
+    // row), so each is issued a tile ahead of the other: a tile's phase 0 stores
+    // the observations loaded during the previous tile, loads the next tile's
+    // rows through indices loaded during the previous tile, and loads the
+    // indices of the tile after that (r6t: one round trip per tile used to stall
+    // phase 0 ~3.7 k cycles).  Entries tid and tid + NT of the [TR][DP] tile;
+    // padding rows are zero (index -1).
+    auto load_idx = [&](int64_t row0, int64_t* xi) {
         const int64_t n = r_end - row0;
         for (int u = 0; u < 2; ++u) {
-            const int e = tid + u * NT, r = e / DP, k = e % DP;
-            xv[u] = (r < n && k < D) ? m.obs[m.idx[row0 + r] * D + k] : 0.0f;
+            const int r = (tid + u * NT) / DP;
+            xi[u] = r < n ? m.idx[row0 + r] : -1;
         }
     };
+    auto load_rows = [&](const int64_t* xi, float* xv) {
+        for (int u = 0; u < 2; ++u) {
+            const int k = (tid + u * NT) % DP;
+            xv[u] = (xi[u] >= 0 && k < D) ? m.obs[xi[u] * D + k] : 0.0f;
+        }
+    };
+    // the loss head's row of this thread (hp == 0: one thread per row)
+    const int hr = tid / 8, hp = tid % 8;
+    auto head_idx = [&](int64_t row0) -> int64_t {
+        return (hp == 0 && hr < r_end - row0) ? m.idx[row0 + hr] : -1;
+    };
     float xv[2];
-    // the first tile's gather (index, then row: two dependent round trips) is
-    // issued before the weight staging, so the two latencies overlap
-    if (r_begin < r_end) load_x(r_begin, xv);
+    int64_t xi[2] = {-1, -1};           // row indices of the next tile's entries
+    int64_t hb = -1, hb_next = -1;      // the head row's index: this tile, the next
+    // the first tile's gather is issued before the weight staging, so the two
+    // latencies overlap; the second tile's indices with it
+    if (r_begin < r_end) {
+        int64_t x0[2];
+        load_idx(r_begin, x0);
+        load_rows(x0, xv);
+        hb = head_idx(r_begin);
+        if (r_begin + TR < r_end) {
+            load_idx(r_begin + TR, xi);
+            hb_next = head_idx(r_begin + TR);
+        }
+    }
     // and so are the advantage partials (summed after it)
     static_assert(NADV <= NT, "one advantage partial per thread");
     const bool norm_adv = m.normalize_advantage && B > 1;
@@ -304,17 +331,20 @@ __global__ __launch_bounds__(NT) void k_mlp_fwd_bwd(RowArgs a) {
     for (int64_t row0 = r_begin; row0 < r_end; row0 += TR) {
         const int nrows = (int)(r_end - row0 < TR ? r_end - row0 : TR);
         for (int u = 0; u < 2; ++u) sX[(tid + u * NT) / DP][(tid + u * NT) % DP] = xv[u];
-        if (row0 + TR < r_end) load_x(row0 + TR, xv);
-        // the loss head's per-row inputs, issued now, used after both layers
-        const int hr = tid / 8, hp = tid % 8;
-        float r_act[NA] = {0.0f, 0.0f, 0.0f}, r_adv = 0.0f, r_olp = 0.0f, r_ret = 0.0f;
-        if (hp == 0 && hr < nrows) {
-            const int64_t b = m.idx[row0 + hr];
-            for (int j = 0; j < NA; ++j) r_act[j] = m.actions[3 * b + j];
-            r_adv = m.advantages[b];
-            r_olp = m.old_log_prob[b];
-            r_ret = m.returns[b];
+        if (row0 + TR < r_end) {
+            load_rows(xi, xv);
+            if (row0 + 2 * TR < r_end) load_idx(row0 + 2 * TR, xi);
         }
+        // the loss head's per-row inputs, issued now, used after both layers
+        float r_act[NA] = {0.0f, 0.0f, 0.0f}, r_adv = 0.0f, r_olp = 0.0f, r_ret = 0.0f;
+        if (hb >= 0) {
+            for (int j = 0; j < NA; ++j) r_act[j] = m.actions[3 * hb + j];
+            r_adv = m.advantages[hb];
+            r_olp = m.old_log_prob[hb];
+            r_ret = m.returns[hb];
+        }
+        hb = hb_next;
+        hb_next = row0 + 2 * TR < r_end ? head_idx(row0 + 2 * TR) : -1;
         __syncthreads();
         // ---- layer 1: h1 = tanh(x W1^T + b1)     (K = 16: 8 steps)
         {
