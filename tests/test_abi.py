@@ -120,3 +120,30 @@ def test_fused_ppo_step_layout(lib):
     assert _lib.N_MLP_TENSORS == len(sizes)
     assert lib.salp_ppo_mlp_num_params(15) == -1 and lib.salp_ppo_mlp_offset(10, 14) == -1
     assert lib.salp_ppo_mlp_grads(None, None) == -1
+
+
+@pytest.mark.parametrize("name,cls", [("SalpParams", _abi.SalpParams), ("SalpRolloutBuffers", _lib.SalpRolloutBuffers),
+                                      ("SalpTraceBuffer", _lib.SalpTraceBuffer),
+                                      ("SalpPolicyRollout", _lib.SalpPolicyRollout),
+                                      ("SalpPpoMinibatch", _lib.SalpPpoMinibatch), ("SalpPpoAdam", _lib.SalpPpoAdam)])
+def test_struct_offsets_match_the_c_compiler(name, cls, tmp_path):
+    """The ctypes mirrors' field offsets and sizes equal what gcc lays out for
+    the header's structs (a field appended, widened or reordered in one place
+    only would hand the library shifted pointers)."""
+    import subprocess
+    fields = [f for f, _ in cls._fields_]
+    src = tmp_path / "o.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "salp.h"\nint main(void) {\n'
+                   + f'    printf("%zu\\n", sizeof({name}));\n'
+                   + "".join(f'    printf("%zu\\n", offsetof({name}, {f}));\n' for f in fields) + "    return 0;\n}\n")
+    exe = tmp_path / "o"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    want = [ctypes.sizeof(cls)] + [getattr(cls, f).offset for f in fields]
+    assert got == want, (name, got, want)
+
+
+def test_ppo_workspace_constants_match_header():
+    text = open(HEADER).read()
+    assert f"#define SALP_PPO_APPLY_WORKSPACE_DOUBLES {_lib.APPLY_WORKSPACE_DOUBLES}" in text
+    assert f"#define SALP_PPO_ADV_PARTIAL_DOUBLES {_lib.ADV_PARTIAL_DOUBLES}" in text
