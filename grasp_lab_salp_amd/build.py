@@ -33,13 +33,33 @@ def up_to_date():
     return all(os.path.getmtime(d) <= t for d in deps())
 
 
+# Per-source scheduler choice: the PPO update's kernels run faster under the
+# max-ILP machine scheduler (update -2 %), the rollout kernels slower (-3 %:
+# profiles/r6_experiments.md r6z), so each source is compiled on its own.
+FILE_FLAGS = {"salp_ppo_mlp.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
+
+
 def build(force=False, verbose=False, extra=()):
     if not force and up_to_date():
         return OUT
-    cmd = [HIPCC, *FLAGS, *extra, "-o", OUT + ".tmp", *SRCS]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+    compile_flags = [f for f in FLAGS if f != "-shared"]
+    with tempfile.TemporaryDirectory(prefix="salp_build_") as tmp:
+        objs = [os.path.join(tmp, os.path.basename(src) + ".o") for src in SRCS]
+        cmds = [[HIPCC, *compile_flags, *FILE_FLAGS.get(os.path.basename(src), []), *extra, "-c", "-o", obj, src]
+                for src, obj in zip(SRCS, objs)]
+        link = [HIPCC, f"--offload-arch={ARCH}", "-fPIC", "-shared", "-o", OUT + ".tmp", *objs]
+        if verbose:
+            for c in cmds + [link]:
+                print(" ".join(c), flush=True)
+        with ThreadPoolExecutor(max_workers=min(len(cmds), os.cpu_count() or 1)) as ex:
+            for r in list(ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), cmds)):
+                if r.returncode:
+                    raise subprocess.CalledProcessError(r.returncode, r.args, r.stdout, r.stderr)
+                if r.stderr and verbose:
+                    print(r.stderr, end="", flush=True)
+        subprocess.run(link, check=True)
     os.replace(OUT + ".tmp", OUT)
     return OUT
 
