@@ -39,17 +39,21 @@ def up_to_date():
 FILE_FLAGS = {"salp_ppo_mlp.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
 
 
-def build(force=False, verbose=False, extra=()):
-    if not force and up_to_date():
+def build(force=False, verbose=False, extra=(), out=None, file_flags=None):
+    """out / file_flags: another output path and per-source flags (A / B builds,
+    tools/build_variant.py); the product build takes neither."""
+    if out is None and not force and up_to_date():
         return OUT
+    out = out or OUT
+    file_flags = FILE_FLAGS if file_flags is None else file_flags
     import tempfile
     from concurrent.futures import ThreadPoolExecutor
     compile_flags = [f for f in FLAGS if f != "-shared"]
     with tempfile.TemporaryDirectory(prefix="salp_build_") as tmp:
         objs = [os.path.join(tmp, os.path.basename(src) + ".o") for src in SRCS]
-        cmds = [[HIPCC, *compile_flags, *FILE_FLAGS.get(os.path.basename(src), []), *extra, "-c", "-o", obj, src]
+        cmds = [[HIPCC, *compile_flags, *file_flags.get(os.path.basename(src), []), *extra, "-c", "-o", obj, src]
                 for src, obj in zip(SRCS, objs)]
-        link = [HIPCC, f"--offload-arch={ARCH}", "-fPIC", "-shared", "-o", OUT + ".tmp", *objs]
+        link = [HIPCC, f"--offload-arch={ARCH}", "-fPIC", "-shared", "-o", out + ".tmp", *objs]
         if verbose:
             for c in cmds + [link]:
                 print(" ".join(c), flush=True)
@@ -60,8 +64,8 @@ def build(force=False, verbose=False, extra=()):
                 if r.stderr and verbose:
                     print(r.stderr, end="", flush=True)
         subprocess.run(link, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
