@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC of the PPO update kernels (k_mlp_fwd_bwd / k_mlp_reduce / k_mlp_apply)
+# PMC of the PPO update kernels (k_mlp_fwd_bwd / k_mlp_reduce / k_mlp_adam)
 # over a short config-5 run (tools/bench_ppo.py, n_steps 32, one iteration),
 # one counter group per pass, kernel trace only.  GRAPHS=0 runs the minibatch
 # steps eagerly (PPO(use_graphs=False)); the kernels are the same.
@@ -30,8 +30,8 @@ for g in ${GROUPS_:-mix lds fetch write}; do
         flops) pass flops SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_TRANS_F32 ;;
     esac
 done
-python3 tools/pmc_kernels_summary.py pmcu_${TAG} k_mlp_fwd_bwd k_mlp_reduce k_mlp_apply k_mlp_adv_sums \
-    k_rollout_pair k_rollout k_gae > gpurun_out/pmcu_${TAG}_summary.json || exit 1
+python3 tools/pmc_kernels_summary.py pmcu_${TAG} k_mlp_fwd_bwd k_mlp_reduce k_mlp_adam k_mlp_apply k_mlp_adv_sums \
+    k_rollout_split k_rollout_pair k_rollout k_gae > gpurun_out/pmcu_${TAG}_summary.json || exit 1
 # the raw per-dispatch CSVs are too large to come back (gpurun_out <= 64 MiB)
 rm -rf gpurun_out/pmcu_${TAG}_*/
 echo "== done $(date +%T)"
